@@ -1,0 +1,267 @@
+"""Benchmark: tracked frames/s (match + GN, 512x512 pointmaps) and BA edges/s.
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+
+A "step" is one FrameTracker.track() of one frame against its keyframe on synthetic MASt3R-shaped
+outputs resident in HBM: fused matching (prep, iterative projection, occlusion, fp16 refine) +
+confidence setup + Sim(3) GN to convergence + keyframe pointmap fusion + selection statistics.
+Workload = BASELINE.json configs[1] (TUM fr1_room, config/calib.yaml: calibrated mode, tracking
+only) at the metric's 512x512 pointmap size. Tracking does not shard (frames are sequential):
+at N > 1 every rank tracks its own sequence ("replicas only", weak scaling). The BA leg shards one
+synthetic factor graph's edges over the ranks (strong scaling, one RCCL all-reduce per iteration).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "lightweight-mast3r-slam_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--mode", choices=["calib", "rays"], default="calib")
+    ap.add_argument("--ring", type=int, default=6, help="distinct synthetic pairs cycled (ring > L3)")
+    ap.add_argument("--ba-kf", type=int, default=64)
+    ap.add_argument("--ba-h", type=int, default=384)
+    ap.add_argument("--ba-w", type=int, default=512)
+    ap.add_argument("--ba-iters", type=int, default=10)
+    ap.add_argument("--no-ba", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def sync_all(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_tracking(args, rank, world, dev):
+    from m3s import _lib
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    H, W = args.height, args.width
+    config["use_calib"] = args.mode == "calib"
+    t0 = time.time()
+    pairs = [make_pair(H, W, seed=1000 * rank + r) for r in range(args.ring)]
+    log(f"[rank {rank}] generated {args.ring} synthetic {H}x{W} pairs in {time.time() - t0:.1f}s")
+    model = SyntheticModel(pairs, dev)
+    kf = Frame(0, (H, W), T_WC=Sim3.Identity(1, device=dev))
+    kf.K = pairs[0]["K"].to(dev)
+    kf.update_pointmap(pairs[0]["Xk"].to(dev), pairs[0]["Ck"].to(dev))
+    kfs = Keyframes()
+    kfs.append(kf)
+    tracker = FrameTracker(model, kfs, dev)
+    lib = _lib.load()
+
+    def step(i):
+        fr = Frame(i, (H, W), T_WC=Sim3(kf.T_WC.data.clone()))
+        return tracker.track(fr)
+
+    for i in range(args.warmup):
+        step(i)
+    iters = []
+    lib.m3s_timing_reset()
+    lib.m3s_timing_enable(1)
+    sync_all(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        new_kf, _, reloc = step(args.warmup + i)
+        iters.append(tracker.last_result.iters)
+        assert not reloc, "synthetic tracking failed"
+    sync_all(world)
+    elapsed = time.perf_counter() - t0
+    lib.m3s_timing_enable(0)
+    kern = {}
+    for name in ("prep_rays", "proj_occlusion", "refine_lin", "track_setup", "gn_iters"):
+        ms, cnt = _lib.c_double(), _lib.c_int()
+        _lib.check(lib.m3s_timing_query(name.encode(), ms, cnt))
+        kern[name] = (ms.value, cnt.value)
+    lib.m3s_timing_reset()
+    elapsed = max_over_ranks(elapsed, world)
+    return elapsed, kern, float(np.mean(iters)), H * W
+
+
+def roofline(kern, N, gn_iters_mean):
+    """Algorithmic bytes / flops per launch / measured HIP-event duration."""
+    per_px_bytes = {
+        "prep_rays": 12 + 96 + 36 + 48,  # X11 + D11 f32 in; rays9 + D11 f16 out
+        "proj_occlusion": 12 + 8 + 36 + 12 + 8 + 1,  # X21, idx_init, rays9, X11 gather, p1, valid
+        "refine_lin": 48 + 96 + 8 + 8,  # D11 f16 centre rows, D21 f32, p1, idx
+        "track_setup": 8 + 1 + 12 + 4 + 4 + 12 + 4 + 4 + 32,  # idx, valid, Xf, Cf, Qff, Xk, Ck, Qkf -> rec
+        "gn_iters": 32 * gn_iters_mean,  # 32 B record per point per iteration
+    }
+    out = {}
+    for k, (ms, cnt) in kern.items():
+        if cnt == 0:
+            continue
+        avg_s = ms / cnt / 1e3
+        out[k] = {"avg_us": avg_s * 1e6, "GBps": per_px_bytes[k] * N / avg_s / 1e9}
+    refine_flops = 245 * 24 * 2 * N  # half products + half adds
+    if "refine_lin" in out:
+        out["refine_lin"]["TFLOPs"] = refine_flops / (out["refine_lin"]["avg_us"] * 1e-6) / 1e12
+    return out
+
+
+def bench_ba(args, rank, world, dev):
+    from m3s.config import config
+    from m3s.dist_ba import HipShard, ba_config, run_sharded, shard_range
+    from m3s.synthetic import make_graph
+
+    G = make_graph(n_kf=args.ba_kf, H=args.ba_h, W=args.ba_w, seed=1, device="cpu")
+    # two-way edges; the reverse maps are a cheap permutation of the forward ones for throughput purposes
+    ii = torch.cat((G["ii"], G["jj"])).to(dev)
+    jj = torch.cat((G["jj"], G["ii"])).to(dev)
+    idx = torch.cat((G["idx"], G["idx"].flip(1))).to(dev).contiguous()
+    valid = torch.cat((G["valid"], G["valid"].flip(1)))[..., 0].to(dev).contiguous()
+    Q = torch.cat((G["Q"], G["Q"].flip(1)))[..., 0].to(dev).contiguous()
+    Xs, Cs = G["Xs"].to(dev).contiguous(), G["Cs"][..., 0].to(dev).contiguous()
+    E = ii.shape[0]
+    e0, e1 = shard_range(E, rank, world)
+    cfg = ba_config("rays", config["local_opt"])
+
+    def run(iters):
+        Twc = G["Twc0"].to(dev).contiguous()
+        shard = HipShard(cfg, Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.0, e0, e1)  # delta 0: no early exit
+        sync_all(world)
+        t0 = time.perf_counter()
+        run_sharded(shard, iters)
+        sync_all(world)
+        return time.perf_counter() - t0, Twc
+
+    run(1)  # warmup
+    el, Twc = run(args.ba_iters)
+    el = max_over_ranks(el, world)
+    return {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
+            "points_per_kf": args.ba_h * args.ba_w, "iters": args.ba_iters, "ms_per_iter": el / args.ba_iters * 1e3,
+            "scaling": "strong", "mode": "rays"}
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement + numpy glue) on the host cores, bounded sample of the same workload."""
+    import oracle.oracle as O
+    from m3s.synthetic import make_pair
+
+    cores = min(16, len(os.sched_getaffinity(0)))
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    H, W = args.height, args.width
+    P = make_pair(H, W, seed=0)
+    X, C, D, Q = (P[k].numpy() for k in ("X", "C", "D", "Q"))
+    Xk, K = P["Xk"].numpy(), P["K"].numpy()
+    N = H * W
+    t0 = time.perf_counter()
+    frames = 0
+    I = np.array([0, 0, 0, 0, 0, 0, 1, 1.0])
+    while True:
+        idx, valid = O.match(X[:1], X[1:], D[:1], D[1:])
+        i = idx[0]
+        Qk = np.sqrt(Q[0].reshape(-1)[i] * Q[1].reshape(-1))
+        v = valid[0, :, 0] & (Qk > 1.5)
+        if args.mode == "calib":
+            Xf = O.backproject_constrain(X[0].reshape(1, -1, 3), K, (H, W))[0][i]
+            u, vv = np.meshgrid(np.arange(W, dtype=np.float32), np.arange(H, dtype=np.float32), indexing="xy")
+            z = Xk[:, 2]
+            vm = z > 1e-6
+            meas = np.stack((u.reshape(-1), vv.reshape(-1), np.log(np.where(vm, z, 1.0))), -1) * vm[:, None]
+            O.track_calib(Xf, Xk, I, I, Qk, v, meas, vm, K, (H, W))
+        else:
+            O.track_rays(X[0].reshape(-1, 3)[i], Xk, I, I, Qk, v)
+        frames += 1
+        if time.perf_counter() - t0 > args.cpu_seconds or frames >= 50:
+            break
+    el = time.perf_counter() - t0
+    return {"value": frames / el, "unit": "tracked frames/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} tracked frames ({H}x{W}, {args.mode}) through oracle/ (C kernels, OpenMP "
+                      f"{cores} threads, + numpy fp64 glue) in {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import __graft_entry__  # noqa: F401  (sys.path)
+
+    elapsed, kern, gn_iters, N = bench_tracking(args, rank, world, dev)
+    total_frames = args.steps * world
+    value = total_frames / elapsed
+    rl = roofline(kern, N, gn_iters)
+    log(f"[rank {rank}] kernels: {json.dumps(rl)}")
+    dom = max(rl.items(), key=lambda kv: kv[1]["avg_us"] * kern[kv[0]][1])
+    name, d = dom
+    if name == "refine_lin":
+        roof = {"kernel": name, "bound": "valu", "achieved": d["TFLOPs"], "peak": VALU_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": d["TFLOPs"] / VALU_F32_PEAK_TFLOPS, "traffic": None}
+    else:
+        roof = {"kernel": name, "bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["GBps"] / HBM_PEAK_GBS, "traffic": None}
+    ba = None
+    if not args.no_ba:
+        ba = bench_ba(args, rank, world, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        rec = {
+            "metric": "tracked frames/s (match+GN, 512x512 pointmaps) @1 GPU; BA edges/s @1/2/4/8",
+            "value": value, "unit": "tracked frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 (refine f16, GN accum f64)",
+            "data": "synthetic MASt3R-shaped pointmaps/descriptors/confidences (no checkpoint, no dataset)",
+            "config": {"workload": f"TUM fr1_room tracking-only, config/calib.yaml "
+                                   f"({'calib' if args.mode == 'calib' else 'rays'} mode), {args.height}x"
+                                   f"{args.width} pointmap pairs, GN to convergence",
+                       "parallelism": f"replicas x{world} (tracking does not shard)",
+                       "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
+            "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
+            "roofline": roof, "cpu_baseline": cpu, "ba": ba,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * m3s.h — C ABI of the MI355X-native MASt3R-SLAM tracking hot path (libm3s.so).
+ *
+ * Plain pointers and sizes only (no torch types). All array pointers are DEVICE pointers on the
+ * current HIP device unless the comment says "host"; `stream` is a hipStream_t passed as void*
+ * (NULL = default stream). Every entry point returns 0 on success or a negative M3S_E* code; the
+ * message of the last failure on the calling thread is available from m3s_last_error().
+ *
+ * Each entry point replaces one operator of the reference's native extension
+ * `mast3r_slam_backends` (bindings /root/reference/mast3r_slam/backend/src/gn.cpp:116-123,
+ * declarations backend/include/gn.h) or fuses a stretch of the reference's Python glue
+ * (mast3r_slam/matching.py, tracker.py). The Python module `mast3r_slam_backends` in
+ * lightweight-mast3r-slam_amd/ binds these through ctypes.
+ */
+#ifndef M3S_H
+#define M3S_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define M3S_ABI_VERSION 1
+
+#define M3S_OK 0
+#define M3S_EINVAL -1  /* bad shape / argument (reference: TORCH_CHECK -> RuntimeError) */
+#define M3S_EHIP -2    /* HIP launch / runtime failure */
+#define M3S_ESPACE -3  /* workspace too small */
+
+int m3s_abi_version(void);
+const char* m3s_last_error(void);
+
+/* Per-kernel HIP-event timing (no reference counterpart; the reference's profiler.py wraps regions
+ * with torch.cuda.synchronize). When enabled, every launch group is bracketed by hipEvents on its
+ * own stream under a name: prep_rays, proj_occlusion, refine_lin, track_setup, gn_iters,
+ * ba_linearize, ba_solve. query synchronises the recorded events. */
+void m3s_timing_enable(int on);
+void m3s_timing_reset(void);
+int m3s_timing_query(const char* name, double* total_ms, int* count);
+
+/* ---------------------------------------------------------------------------------------------
+ * Reference operators (drop-in for mast3r_slam_backends.*)
+ * ------------------------------------------------------------------------------------------- */
+
+/* iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh)
+ *   -> [p_new, converged]                                   gn.cpp:84-99, gn.h:89-95,
+ *                                                           matching_kernels.cu:119-316
+ * rays (B,H,W,C=9) f32, pts (B,N,3) f32, p_init (B,N,2) f32 -> p_new (B,N,2) f32, converged (B,N) u8 */
+int m3s_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new, uint8_t* converged,
+                  int B, int H, int W, int C, int N, int max_iter, float lambda_init, float cost_thresh,
+                  void* stream);
+
+/* refine_matches(D11, D21, p1, radius, dilation_max) -> [p1_new]
+ *                                                           gn.cpp:101-114, gn.h:112-117,
+ *                                                           matching_kernels.cu:25-116
+ * dtype 0 = f16 (c10::Half step rounding), 1 = f32. D11 (B,H,W,F), D21 (B,N,F), p1 (B,N,2) i64
+ * -> p1_new (B,N,2) i64 */
+int m3s_refine_matches(int dtype, const void* D11, const void* D21, const int64_t* p1, int64_t* p1_new, int B,
+                       int H, int W, int F, int N, int radius, int dilation_max, void* stream);
+
+/* gauss_newton_{points,rays,calib}(Twc, Xs, Cs, [K,] ii, jj, idx_ii2jj, valid_match, Q, ...) -> [dx]
+ *                                                           gn.cpp:3-82, gn.h:22-87,
+ *                                                           gn_kernels.cu:725-811, 1140-1228, 1546-1637
+ * Twc (Kp,8) f32 is updated IN PLACE (as the reference). Xs (Kp,N,3), Cs (Kp,N) f32; ii, jj (E) i64
+ * global keyframe ids (remapped to dense ranks internally, gn_kernels.cu:161-170); idx (E,N) i64;
+ * valid (E,N) u8; Q (E,N) f32. dx_out ((Kp-1),7) f32 receives the last step. iters_out (host,
+ * nullable) receives the iteration count. The workspace must hold m3s_ba_workspace_size() bytes. */
+typedef struct m3s_ba_config {
+  int mode;          /* 0 points, 1 rays, 2 calib */
+  float sigma_a;     /* sigma_point | sigma_ray | sigma_pixel */
+  float sigma_b;     /* -           | sigma_dist | sigma_depth */
+  float C_thresh, Q_thresh;
+  float fx, fy, cx, cy; /* calib: K[0,0], K[1,1], K[0,2], K[1,2] (host values) */
+  int height, width, pixel_border;
+  float z_eps;
+} m3s_ba_config;
+
+size_t m3s_ba_workspace_size(int Kp, int N, int E);
+int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                     const int64_t* ii, const int64_t* jj, int E, const int64_t* idx, const uint8_t* valid,
+                     const float* Q, int max_iter, float delta_thresh, float* dx_out, int* iters_out,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Split BA for edge-sharded multi-GPU runs (no reference counterpart).
+ * plan: rank remap + block-sparse assembly pattern for ALL E edges, shard = edges [e0, e1).
+ * Per iteration: m3s_ba_linearize (this shard's rows of the (E,36) f64 edge-sum table), then the
+ * caller all-reduces that table (offset/size from m3s_ba_edge_sums), then m3s_ba_solve. */
+typedef struct m3s_ba_plan { unsigned char opaque[768]; } m3s_ba_plan;
+int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                     const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                     const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out, void* workspace,
+                     size_t workspace_bytes, m3s_ba_plan* plan, void* stream);
+int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count);
+int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
+int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);
+int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /* syncs the stream */
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused operators (replace stretches of the reference's Python glue)
+ * ------------------------------------------------------------------------------------------- */
+
+/* match(X11, X21, D11, D21, idx_init) -> (idx_1_to_2, valid_match2)     matching.py:8-90
+ * X11, X21 (B,H,W,3) f32; D11, D21 (B,H,W,F) f32 (F % 8 == 0, F in {16,24,32}); idx_init (B,N) i64
+ * or NULL (identity). idx_out (B,N) i64; valid_out (B,N) u8. Parameters = config `matching.*`. */
+size_t m3s_match_workspace_size(int B, int H, int W, int F);
+int m3s_match(const float* X11, const float* X21, const float* D11, const float* D21, const int64_t* idx_init,
+              int64_t* idx_out, uint8_t* valid_out, int B, int H, int W, int F, int max_iter, float lambda_init,
+              float cost_thresh, float dist_thresh, int radius, int dilation_max, void* workspace,
+              size_t workspace_bytes, void* stream);
+
+/* FrameTracker.track post-matching stretch (tracker.py:35-114): setup, Sim(3) GN to convergence
+ * (rays: opt_pose_ray_dist_sim3 :173-214; calib: opt_pose_calib_sim3 :216-266), keyframe pointmap
+ * fusion (frame.py:74-77) and the keyframe-selection statistics. */
+#define M3S_TRACK_OK 1
+#define M3S_TRACK_MAX_ITERS 2
+#define M3S_TRACK_CHOLESKY_FAILED 3
+#define M3S_TRACK_SKIPPED 4
+
+typedef struct m3s_track_config {
+  int mode;           /* 0 rays (use_calib False), 1 calib */
+  int max_iters;      /* tracking.max_iters */
+  float C_conf, Q_conf, min_match_frac;
+  float sigma_a;      /* sigma_ray | sigma_pixel */
+  float sigma_b;      /* sigma_dist | sigma_depth */
+  float huber_k, rel_error, delta_norm;
+  float pixel_border, depth_eps;
+  float K[9];         /* calib intrinsics, row-major (host values) */
+  int H, W;
+} m3s_track_config;
+
+typedef struct m3s_track_inputs {
+  const int64_t* idx_f2k;      /* (N) */
+  const uint8_t* valid_match;  /* (N) */
+  const float* Xf;             /* (N,3) frame X_canon */
+  const float* Cf;             /* (N)   frame C (sum) */
+  float Nf;                    /* frame fusion count */
+  const float* Qff;            /* (N) */
+  const float* Xk;             /* (N,3) keyframe X_canon */
+  const float* Ck;             /* (N)   keyframe C (sum) */
+  float Nk;                    /* keyframe fusion count */
+  const float* Qkf;            /* (N) */
+  const float* T_WCf;          /* (8) device */
+  const float* T_WCk;          /* (8) device */
+  /* direct = 1: the opt_pose_* surface (tracker.py:173,216). idx_f2k is ignored (identity),
+   * Qff holds Qk, valid_match holds valid_opt, Xf is already gathered (and constrained in calib
+   * mode), meas_k (N,3) / valid_meas_k (N) are given; Cf, Ck, Qkf are unused. */
+  int direct;
+  const float* meas_k;
+  const uint8_t* valid_meas_k;
+} m3s_track_inputs;
+
+typedef struct m3s_track_fuse_args {
+  float* Xk_canon;    /* (N,3) keyframe X_canon, updated in place; NULL = no fusion */
+  float* Ck_sum;      /* (N)   keyframe C, updated in place */
+  const float* Xkf;   /* (N,3) model output: keyframe points in the frame's camera */
+  const float* Ckf;   /* (N) */
+} m3s_track_fuse_args;
+
+typedef struct m3s_track_result {
+  float T_WCf[8];
+  float T_CkCf[8];
+  double cost;
+  int iters, status, n_valid_opt, n_valid_kf, n_unique, N;
+} m3s_track_result;
+
+size_t m3s_track_workspace_size(int N);
+int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s_track_fuse_args* fuse,
+              int first_chunk, float* T_out_dev /* (16) nullable: T_WCf | T_CkCf on device */,
+              m3s_track_result* result /* host */, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* M3S_H */

@@ -1,0 +1,574 @@
+// C ABI of libm3s.so (include/m3s.h): argument validation, workspace carving, host-side planning
+// (rank remap, assembly pattern) and launch sequencing. Kernels live in matching.hip, track.hip
+// and ba.hip. No torch types anywhere below this line.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/m3s.h"
+#include "m3s_ba.h"
+#include "m3s_track.h"
+
+extern "C" {
+hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, hipStream_t);
+hipError_t m3s_launch_iter_proj(const float*, const float*, const float*, float*, uint8_t*, int, int, int, int, int,
+                                float, float, hipStream_t);
+hipError_t m3s_launch_proj_occlusion(const float*, const float*, const float*, const int64_t*, int*, uint8_t*, int, int,
+                                     int, int, float, float, float, hipStream_t);
+hipError_t m3s_launch_refine_f16(const void*, const void*, const int64_t*, int64_t*, int, int, int, int, int, int, int,
+                                 hipStream_t);
+hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int64_t*, int, int, int, int, int, int,
+                                 int, hipStream_t);
+hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*, int, int, int, int, int, int,
+                                 hipStream_t);
+hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
+hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, hipStream_t);
+hipError_t m3s_launch_fuse(const void*, float*, float*, const float*, const float*, int, hipStream_t);
+hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, hipStream_t);
+hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
+hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  return fail(M3S_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+  template <typename T>
+  T* take(size_t count) {
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += align256(sizeof(T) * (count > 0 ? count : 1));
+    return p;
+  }
+};
+
+#define M3S_CHECK(cond, msg)                 \
+  do {                                       \
+    if (!(cond)) return fail(M3S_EINVAL, msg); \
+  } while (0)
+
+#define HIP_TRY(expr, where)                \
+  do {                                      \
+    hipError_t _e = (expr);                 \
+    if (_e != hipSuccess) return hip_fail(_e, where); \
+  } while (0)
+
+// ---- per-kernel HIP-event timing (bench.py reads it; off by default, zero cost when off) ----
+struct TimedSpan {
+  hipEvent_t a, b;
+};
+std::map<std::string, std::vector<TimedSpan>> g_spans;
+bool g_timing = false;
+
+struct Span {
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  const char* name;
+  Span(const char* n, hipStream_t st) : s(st), name(n) {
+    if (!g_timing) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      a = b = nullptr;
+      return;
+    }
+    (void)hipEventRecord(a, s);
+  }
+  ~Span() {
+    if (!g_timing || a == nullptr) return;
+    (void)hipEventRecord(b, s);
+    g_spans[name].push_back({a, b});
+  }
+};
+
+}  // namespace
+
+extern "C" void m3s_timing_enable(int on) { g_timing = on != 0; }
+
+extern "C" void m3s_timing_reset(void) {
+  for (auto& kv : g_spans)
+    for (auto& sp : kv.second) {
+      (void)hipEventDestroy(sp.a);
+      (void)hipEventDestroy(sp.b);
+    }
+  g_spans.clear();
+}
+
+// total milliseconds and span count recorded under `name` (synchronises the recorded events)
+extern "C" int m3s_timing_query(const char* name, double* total_ms, int* count) {
+  *total_ms = 0.0;
+  *count = 0;
+  auto it = g_spans.find(name);
+  if (it == g_spans.end()) return M3S_OK;
+  for (auto& sp : it->second) {
+    HIP_TRY(hipEventSynchronize(sp.b), "timing sync");
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, sp.a, sp.b), "timing elapsed");
+    *total_ms += ms;
+    *count += 1;
+  }
+  return M3S_OK;
+}
+
+extern "C" int m3s_abi_version(void) { return M3S_ABI_VERSION; }
+extern "C" const char* m3s_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------
+// reference operators
+// ------------------------------------------------------------------------------------------
+extern "C" int m3s_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
+                             uint8_t* converged, int B, int H, int W, int C, int N, int max_iter, float lambda_init,
+                             float cost_thresh, void* stream) {
+  M3S_CHECK(B >= 0 && N >= 0 && H >= 3 && W >= 3, "iter_proj: image must be at least 3x3");
+  M3S_CHECK(C == 9, "iter_proj: rays_img_with_grad must have 9 channels (ray, gx, gy)");
+  M3S_CHECK(max_iter >= 0, "iter_proj: max_iter must be >= 0");
+  if (B == 0 || N == 0) return M3S_OK;
+  M3S_CHECK(rays && pts && p_init && p_new && converged, "iter_proj: null pointer");
+  HIP_TRY(m3s_launch_iter_proj(rays, pts, p_init, p_new, converged, B, H, W, N, max_iter, lambda_init, cost_thresh,
+                               (hipStream_t)stream),
+          "iter_proj launch");
+  return M3S_OK;
+}
+
+extern "C" int m3s_refine_matches(int dtype, const void* D11, const void* D21, const int64_t* p1, int64_t* p1_new,
+                                  int B, int H, int W, int F, int N, int radius, int dilation_max, void* stream) {
+  M3S_CHECK(B >= 0 && N >= 0 && H >= 1 && W >= 1, "refine_matches: bad shape");
+  M3S_CHECK(radius >= 0 && dilation_max >= 0, "refine_matches: radius/dilation_max must be >= 0");
+  if (B == 0 || N == 0) return M3S_OK;
+  M3S_CHECK(D11 && D21 && p1 && p1_new, "refine_matches: null pointer");
+  if (dtype == 0) {
+    M3S_CHECK(F == 16 || F == 24 || F == 32, "refine_matches: f16 path supports F in {16,24,32}");
+    HIP_TRY(m3s_launch_refine_f16(D11, D21, p1, p1_new, B, H, W, F, N, radius, dilation_max, (hipStream_t)stream),
+            "refine_matches launch");
+  } else if (dtype == 1) {
+    M3S_CHECK(F >= 1, "refine_matches: F must be >= 1");
+    HIP_TRY(m3s_launch_refine_f32((const float*)D11, (const float*)D21, p1, p1_new, B, H, W, F, N, radius,
+                                  dilation_max, (hipStream_t)stream),
+            "refine_matches launch");
+  } else {
+    return fail(M3S_EINVAL, "refine_matches: dtype must be 0 (f16) or 1 (f32)");
+  }
+  return M3S_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// fused match
+// ------------------------------------------------------------------------------------------
+static size_t match_carve(Carver& c, int B, int H, int W, int F, float** rays9, void** D11h, int** p1) {
+  *rays9 = c.take<float>((size_t)B * H * W * 9);
+  *D11h = c.take<uint16_t>((size_t)B * H * W * F);
+  *p1 = c.take<int>((size_t)B * H * W * 2);
+  return c.off;
+}
+
+extern "C" size_t m3s_match_workspace_size(int B, int H, int W, int F) {
+  Carver c(nullptr);
+  float* r;
+  void* d;
+  int* p;
+  return match_carve(c, B, H, W, F, &r, &d, &p);
+}
+
+extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, const float* D21,
+                         const int64_t* idx_init, int64_t* idx_out, uint8_t* valid_out, int B, int H, int W, int F,
+                         int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int radius,
+                         int dilation_max, void* workspace, size_t workspace_bytes, void* stream) {
+  M3S_CHECK(B >= 1 && H >= 3 && W >= 3, "match: image must be at least 3x3");
+  M3S_CHECK(F == 16 || F == 24 || F == 32, "match: descriptor dim must be 16, 24 or 32");
+  M3S_CHECK(X11 && X21 && D11 && D21 && idx_out && valid_out, "match: null pointer");
+  M3S_CHECK(max_iter >= 0 && radius >= 0 && dilation_max >= 0, "match: negative parameter");
+  if (workspace_bytes < m3s_match_workspace_size(B, H, W, F)) return fail(M3S_ESPACE, "match: workspace too small");
+  Carver c(workspace);
+  float* rays9;
+  void* D11h;
+  int* p1;
+  match_carve(c, B, H, W, F, &rays9, &D11h, &p1);
+  hipStream_t s = (hipStream_t)stream;
+  {
+    Span sp("prep_rays", s);
+    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 ? D11 : nullptr, D11h, B, H, W, F, s), "match prep launch");
+  }
+  {
+    Span sp("proj_occlusion", s);
+    HIP_TRY(m3s_launch_proj_occlusion(rays9, X11, X21, idx_init, p1, valid_out, B, H, W, max_iter, lambda_init,
+                                      cost_thresh, dist_thresh, s),
+            "match proj launch");
+  }
+  // radius == 0: the refine loop is empty and the kernel only writes idx = pixel_to_lin(p1)
+  // (matching.py:78-88); D11h is never read then.
+  {
+    Span sp("refine_lin", s);
+    HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, s),
+            "match refine launch");
+  }
+  return M3S_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// tracking
+// ------------------------------------------------------------------------------------------
+static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }
+
+static size_t track_carve(Carver& c, int N, TrackState** st, uint32_t** bitmap, double** partials, float** rec) {
+  *st = c.take<TrackState>(1);
+  *bitmap = c.take<uint32_t>((size_t)(N + 31) / 32);
+  *partials = c.take<double>((size_t)track_nparts(N) * 40);
+  *rec = c.take<float>((size_t)N * 8);
+  return c.off;
+}
+
+extern "C" size_t m3s_track_workspace_size(int N) {
+  Carver c(nullptr);
+  TrackState* st;
+  uint32_t* bm;
+  double* pa;
+  float* rec;
+  return track_carve(c, N, &st, &bm, &pa, &rec);
+}
+
+extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s_track_fuse_args* fuse,
+                         int first_chunk, float* T_out_dev, m3s_track_result* result, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  M3S_CHECK(in && cfg && result, "track: null argument");
+  const int N = cfg->H * cfg->W;
+  M3S_CHECK(cfg->H >= 1 && cfg->W >= 1, "track: bad image size");
+  M3S_CHECK(cfg->mode == 0 || cfg->mode == 1, "track: mode must be 0 (rays) or 1 (calib)");
+  M3S_CHECK(cfg->max_iters >= 1, "track: max_iters must be >= 1");
+  if (in->direct) {
+    M3S_CHECK(in->valid_match && in->Xf && in->Qff && in->T_WCf && in->T_WCk, "track: null input pointer");
+    M3S_CHECK(cfg->mode == 0 ? in->Xk != nullptr : (in->meas_k && in->valid_meas_k),
+              "track direct: rays needs Xk, calib needs meas_k/valid_meas_k");
+  } else {
+    M3S_CHECK(in->idx_f2k && in->valid_match && in->Xf && in->Cf && in->Qff && in->Xk && in->Ck && in->Qkf &&
+                  in->T_WCf && in->T_WCk,
+              "track: null input pointer");
+    M3S_CHECK(in->Nf > 0 && in->Nk > 0, "track: fusion counts must be positive");
+  }
+  if (workspace_bytes < m3s_track_workspace_size(N)) return fail(M3S_ESPACE, "track: workspace too small");
+  Carver c(workspace);
+  TrackArgs a;
+  TrackState* st;
+  track_carve(c, N, &st, &a.bitmap, &a.partials, &a.rec);
+  a.state = st;
+  a.idx = in->idx_f2k;
+  a.valid_match = in->valid_match;
+  a.Xf = in->Xf;
+  a.Cf = in->Cf;
+  a.Qff = in->Qff;
+  a.Xk = in->Xk;
+  a.Ck = in->Ck;
+  a.Qkf = in->Qkf;
+  a.meas_k = in->meas_k;
+  a.valid_meas = in->valid_meas_k;
+  TrackParams p;
+  memset(&p, 0, sizeof(p));
+  p.N = N;
+  p.H = cfg->H;
+  p.W = cfg->W;
+  p.mode = cfg->mode;
+  p.Nf = in->direct ? 1.0f : in->Nf;
+  p.Nk = in->direct ? 1.0f : in->Nk;
+  p.direct = in->direct != 0;
+  p.C_conf = cfg->C_conf;
+  p.Q_conf = cfg->Q_conf;
+  p.min_match_frac = in->direct ? -1.0f : cfg->min_match_frac;  // opt_pose_* never skips
+  p.c_a = (float)(1.0 / (double)cfg->sigma_a);  // tracker.py:175-176: python 1/sigma cast to float32
+  p.c_b = (float)(1.0 / (double)cfg->sigma_b);
+  p.huber_k = cfg->huber_k;
+  p.rel_error = cfg->rel_error;
+  p.delta_norm = cfg->delta_norm;
+  p.max_iters = cfg->max_iters;
+  p.pixel_border = cfg->pixel_border;
+  p.depth_eps = cfg->depth_eps;
+  for (int i = 0; i < 9; i++) p.K[i] = cfg->K[i];
+  p.fx = cfg->K[0];
+  p.fy = cfg->K[4];
+  p.cx = cfg->K[2];
+  p.cy = cfg->K[5];
+  if (p.mode == 1) M3S_CHECK(p.fx != 0.0f && p.fy != 0.0f, "track: calib mode needs K");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t bitmap_bytes = ((size_t)(N + 31) / 32) * 4;
+  HIP_TRY(hipMemsetAsync(st, 0, sizeof(TrackState), s), "track memset");
+  HIP_TRY(hipMemsetAsync(a.bitmap, 0, bitmap_bytes, s), "track memset");
+  HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, s), "track init launch");
+  {
+    Span sp("track_setup", s);
+    HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
+  }
+  const int nparts = track_nparts(N);
+  int launched = 0;
+  int chunk = std::max(1, std::min(first_chunk, p.max_iters));
+  TrackState hs;
+  for (;;) {
+    {
+      Span sp("gn_iters", s);
+      HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, chunk, s), "track iterate launch");
+    }
+    launched += chunk;
+    if (T_out_dev) {
+      HIP_TRY(hipMemcpyAsync(T_out_dev, st->T_WCf, 8 * sizeof(float), hipMemcpyDeviceToDevice, s), "track copy");
+      HIP_TRY(hipMemcpyAsync(T_out_dev + 8, st->T, 8 * sizeof(float), hipMemcpyDeviceToDevice, s), "track copy");
+    }
+    HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
+    HIP_TRY(hipStreamSynchronize(s), "track sync");
+    if (hs.done || launched >= p.max_iters) break;
+    chunk = std::min(8, p.max_iters - launched);
+  }
+  // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) only after a successful solve (tracker.py:91-101);
+  // enqueued after the last readback, stream order makes it visible to every later consumer.
+  if (fuse && fuse->Xk_canon && (hs.status == M3S_TRACK_OK || hs.status == M3S_TRACK_MAX_ITERS))
+    HIP_TRY(m3s_launch_fuse(st, fuse->Xk_canon, fuse->Ck_sum, fuse->Xkf, fuse->Ckf, N, s), "track fuse launch");
+  memcpy(result->T_WCf, hs.T_WCf, sizeof(result->T_WCf));
+  memcpy(result->T_CkCf, hs.T, sizeof(result->T_CkCf));
+  result->cost = hs.last_cost;
+  result->iters = hs.iter;
+  result->status = hs.status;
+  result->n_valid_opt = hs.n_valid_opt;
+  result->n_valid_kf = hs.n_valid_kf;
+  result->n_unique = hs.n_unique;
+  result->N = N;
+  return M3S_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// bundle adjustment
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct BaPlanImpl {
+  BaArgs a;
+  BaParams p;
+  int Kp, N, E, e0, e1;
+  int nblocks, nrhs;
+  float delta_thresh;
+  size_t edge_sums_off, edge_sums_bytes;
+  void* ws;
+};
+static_assert(sizeof(BaPlanImpl) <= sizeof(m3s_ba_plan), "m3s_ba_plan too small");
+
+int ba_chunks(int N, int E) {
+  const int want = (2048 + std::max(E, 1) - 1) / std::max(E, 1);
+  const int cap = std::max(1, (N + 4095) / 4096);
+  return std::max(1, std::min(want, cap));
+}
+
+size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* es_off) {
+  const int n = std::max(0, (Kp - 1) * 7);
+  const int nb_max = Kp + E;
+  a->ii_rank = c.take<int>(E);
+  a->jj_rank = c.take<int>(E);
+  a->partials = c.take<double>((size_t)E * chunks * 36);
+  *es_off = c.off;
+  a->edge_sums = c.take<double>((size_t)E * 36);
+  a->blk_row = c.take<int>(nb_max);
+  a->blk_col = c.take<int>(nb_max);
+  a->blk_ptr = c.take<int>(nb_max + 1);
+  a->blk_ent = c.take<int>((size_t)4 * E);
+  a->rhs_ptr = c.take<int>(Kp + 1);
+  a->rhs_ent = c.take<int>((size_t)2 * E);
+  a->H = c.take<double>((size_t)(n + 1) * std::max(n, 1));
+  a->x = c.take<double>(std::max(n, 1));
+  a->dx = c.take<float>(std::max(n, 1));
+  a->info = c.take<int>(4);
+  a->done = a->info + 1;
+  a->iters = a->info + 2;
+  return c.off;
+}
+
+}  // namespace
+
+extern "C" size_t m3s_ba_workspace_size(int Kp, int N, int E) {
+  Carver c(nullptr);
+  BaArgs a;
+  size_t off;
+  return ba_carve(c, Kp, N, E, ba_chunks(N, E), &a, &off);
+}
+
+extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                                const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                                const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                                void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(cfg && plan, "ba: null argument");
+  M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
+  M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
+  M3S_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "ba: bad shard range");
+  if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
+                                "ba calib: height*width must equal the points per keyframe");
+  if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  BaPlanImpl P;
+  memset(&P, 0, sizeof(P));
+  const int chunks = ba_chunks(N, E);
+  Carver c(workspace);
+  ba_carve(c, Kp, N, E, chunks, &P.a, &P.edge_sums_off);
+  P.edge_sums_bytes = (size_t)E * 36 * sizeof(double);
+  // rank remap (gn_kernels.cu:161-170): unique(cat(ii,jj)) sorted; searchsorted; pin = 1 for rows
+  std::vector<int64_t> hii(E), hjj(E);
+  if (E > 0) {
+    HIP_TRY(hipMemcpyAsync(hii.data(), ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba ii readback");
+    HIP_TRY(hipMemcpyAsync(hjj.data(), jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba jj readback");
+    HIP_TRY(hipStreamSynchronize(s), "ba sync");
+  }
+  std::vector<int64_t> u(hii);
+  u.insert(u.end(), hjj.begin(), hjj.end());
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  if ((int)u.size() > Kp) return fail(M3S_EINVAL, "ba: more unique keyframe ids in ii/jj than poses in Twc");
+  std::vector<int> ri(E), rj(E);
+  for (int e = 0; e < E; e++) {
+    ri[e] = (int)(std::lower_bound(u.begin(), u.end(), hii[e]) - u.begin());
+    rj[e] = (int)(std::lower_bound(u.begin(), u.end(), hjj[e]) - u.begin());
+  }
+  // assembly pattern (SparseBlock::update_lhs/rhs, gn_kernels.cu:71-113), lower blocks only,
+  // contributions in edge order. Off-diagonal blocks carry -M (H_ij = -H_jj), diagonal +M.
+  const int nopt = Kp - 1;
+  std::map<std::pair<int, int>, std::vector<int>> blocks;
+  std::vector<std::vector<int>> rhs(std::max(nopt, 0));
+  for (int e = 0; e < E; e++) {
+    const int io = ri[e] - 1, jo = rj[e] - 1;
+    const int rows[4] = {io, io, jo, jo}, cols[4] = {io, jo, io, jo};
+    const int neg[4] = {0, 1, 1, 0};
+    for (int k = 0; k < 4; k++) {
+      if (rows[k] < 0 || cols[k] < 0 || rows[k] < cols[k]) continue;
+      blocks[{rows[k], cols[k]}].push_back(e * 2 + neg[k]);
+    }
+    if (io >= 0) rhs[io].push_back(e * 2 + 1);  // g_i = -g_j
+    if (jo >= 0) rhs[jo].push_back(e * 2 + 0);
+  }
+  std::vector<int> brow, bcol, bptr{0}, bent, rptr{0}, rent;
+  for (auto& kv : blocks) {
+    brow.push_back(kv.first.first);
+    bcol.push_back(kv.first.second);
+    bent.insert(bent.end(), kv.second.begin(), kv.second.end());
+    bptr.push_back((int)bent.size());
+  }
+  for (int r = 0; r < nopt; r++) {
+    rent.insert(rent.end(), rhs[r].begin(), rhs[r].end());
+    rptr.push_back((int)rent.size());
+  }
+  auto h2d = [&](const void* dst, const void* src, size_t bytes) -> hipError_t {
+    if (bytes == 0) return hipSuccess;
+    return hipMemcpyAsync(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice, s);
+  };
+  // shard-local rank arrays
+  HIP_TRY(h2d(P.a.ii_rank, ri.data() + e0, sizeof(int) * (e1 - e0)), "ba upload");
+  HIP_TRY(h2d(P.a.jj_rank, rj.data() + e0, sizeof(int) * (e1 - e0)), "ba upload");
+  HIP_TRY(h2d(P.a.blk_row, brow.data(), sizeof(int) * brow.size()), "ba upload");
+  HIP_TRY(h2d(P.a.blk_col, bcol.data(), sizeof(int) * bcol.size()), "ba upload");
+  HIP_TRY(h2d(P.a.blk_ptr, bptr.data(), sizeof(int) * bptr.size()), "ba upload");
+  HIP_TRY(h2d(P.a.blk_ent, bent.data(), sizeof(int) * bent.size()), "ba upload");
+  HIP_TRY(h2d(P.a.rhs_ptr, rptr.data(), sizeof(int) * rptr.size()), "ba upload");
+  HIP_TRY(h2d(P.a.rhs_ent, rent.data(), sizeof(int) * rent.size()), "ba upload");
+  HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
+  HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");
+  HIP_TRY(hipStreamSynchronize(s), "ba upload sync");  // host vectors die at return
+  P.a.Twc = Twc;
+  P.a.Xs = Xs;
+  P.a.Cs = Cs;
+  P.a.idx = idx;
+  P.a.valid = valid;
+  P.a.Q = Q;
+  P.p.mode = cfg->mode;
+  P.p.N = N;
+  P.p.chunks = chunks;
+  P.p.edge_offset = e0;
+  // gn_kernels.cu:546, 905-906, 1341-1342: const float sigma_inv = 1.0/sigma (double division)
+  P.p.inv_a = (float)(1.0 / (double)cfg->sigma_a);
+  P.p.inv_b = cfg->mode == 0 ? 0.0f : (float)(1.0 / (double)cfg->sigma_b);
+  P.p.C_thresh = cfg->C_thresh;
+  P.p.Q_thresh = cfg->Q_thresh;
+  P.p.fx = cfg->fx;
+  P.p.fy = cfg->fy;
+  P.p.cx = cfg->cx;
+  P.p.cy = cfg->cy;
+  P.p.H = cfg->height;
+  P.p.W = cfg->width;
+  P.p.pixel_border = cfg->pixel_border;
+  P.p.z_eps = cfg->z_eps;
+  P.Kp = Kp;
+  P.N = N;
+  P.E = E;
+  P.e0 = e0;
+  P.e1 = e1;
+  P.nblocks = (int)brow.size();
+  P.nrhs = nopt;
+  P.delta_thresh = delta_thresh;
+  P.ws = workspace;
+  P.a.dx = dx_out ? dx_out : P.a.dx;
+  memcpy(plan->opaque, &P, sizeof(P));
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count) {
+  M3S_CHECK(plan && byte_offset && byte_count, "ba: null argument");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  *byte_offset = P->edge_sums_off;
+  *byte_count = P->edge_sums_bytes;
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(plan, "ba: null plan");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  hipStream_t s = (hipStream_t)stream;
+  // a shard writes only its own rows: clear the rest so the caller's all-reduce sums fresh rows
+  if ((P->e0 > 0 || P->e1 < P->E) && P->edge_sums_bytes > 0)
+    HIP_TRY(hipMemsetAsync(P->a.edge_sums, 0, P->edge_sums_bytes, s), "ba memset");
+  Span sp("ba_linearize", s);
+  HIP_TRY(m3s_launch_ba_lin(&P->a, &P->p, P->e1 - P->e0, s), "ba linearize launch");
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_solve(const m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(plan, "ba: null plan");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  Span sp("ba_solve", (hipStream_t)stream);
+  HIP_TRY(m3s_launch_ba_solve(&P->a, P->Kp, P->nblocks, P->nrhs, P->delta_thresh, (hipStream_t)stream),
+          "ba solve launch");
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream) {
+  M3S_CHECK(plan && iters_out, "ba: null argument");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(iters_out, P->a.iters, sizeof(int), hipMemcpyDeviceToHost, s), "ba readback");
+  HIP_TRY(hipStreamSynchronize(s), "ba sync");
+  return M3S_OK;
+}
+
+extern "C" int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                                const int64_t* ii, const int64_t* jj, int E, const int64_t* idx,
+                                const uint8_t* valid, const float* Q, int max_iter, float delta_thresh, float* dx_out,
+                                int* iters_out, void* workspace, size_t workspace_bytes, void* stream) {
+  M3S_CHECK(max_iter >= 0, "ba: max_iter must be >= 0");
+  m3s_ba_plan plan;
+  int rc = m3s_ba_make_plan(cfg, Twc, Xs, Cs, Kp, N, ii, jj, E, 0, E, idx, valid, Q, delta_thresh, dx_out, workspace,
+                            workspace_bytes, &plan, stream);
+  if (rc != M3S_OK) return rc;
+  if (dx_out && Kp > 1)
+    HIP_TRY(hipMemsetAsync(dx_out, 0, sizeof(float) * (size_t)(Kp - 1) * 7, (hipStream_t)stream), "ba memset");
+  for (int it = 0; it < max_iter; it++) {
+    if ((rc = m3s_ba_linearize(&plan, stream)) != M3S_OK) return rc;
+    if ((rc = m3s_ba_solve(&plan, stream)) != M3S_OK) return rc;
+  }
+  if (iters_out) return m3s_ba_iterations(&plan, iters_out, stream);
+  return M3S_OK;
+}

@@ -1,0 +1,55 @@
+// Internal (non-ABI) structs shared by track.hip and abi.cpp. The public C ABI is include/m3s.h.
+#pragma once
+#include <stdint.h>
+
+#define M3S_TRACK_RUNNING 0
+#define M3S_TRACK_OK 1
+#define M3S_TRACK_MAX_ITERS 2
+#define M3S_TRACK_CHOLESKY_FAILED 3
+#define M3S_TRACK_SKIPPED 4
+
+// Device-resident GN state (one per tracked frame). Layout mirrored by m3s/_track.py (M3S_TRACK_STATE_*).
+struct TrackState {
+  float T[8];      // T_CkCf (current estimate)
+  float T_WCk[8];  // keyframe pose
+  float T_WCf[8];  // output: T_WCk * T_CkCf
+  double old_cost;
+  double last_cost;
+  int iter;
+  int done;
+  int status;
+  int n_valid_opt;
+  int n_valid_kf;
+  int n_unique;
+  int pad[2];
+};
+
+struct TrackParams {
+  int N, H, W, mode;  // mode 0 = rays (opt_pose_ray_dist_sim3), 1 = calib (opt_pose_calib_sim3)
+  float Nf, Nk;       // frame / keyframe fusion counts (get_average_conf divisors)
+  float C_conf, Q_conf, min_match_frac;
+  float c_a, c_b;     // float32(1/sigma_ray|pixel), float32(1/sigma_dist|depth)
+  float huber_k, rel_error, delta_norm;
+  int max_iters;
+  float pixel_border, depth_eps;
+  float fx, fy, cx, cy;
+  float K[9];
+  int direct;  // opt_pose_* surface: inputs already gathered / constrained (see m3s.h)
+};
+
+struct TrackArgs {
+  const int64_t* idx;          // (N) idx_f2k
+  const uint8_t* valid_match;  // (N)
+  const float* Xf;             // (N,3) frame X_canon
+  const float* Cf;             // (N) frame C (sum)
+  const float* Qff;            // (N)
+  const float* Xk;             // (N,3) keyframe X_canon
+  const float* Ck;             // (N) keyframe C (sum)
+  const float* Qkf;            // (N)
+  const float* meas_k;         // (N,3) direct calib only
+  const uint8_t* valid_meas;   // (N)   direct calib only
+  float* rec;                 // (N,8) per-point GN record (workspace)
+  uint32_t* bitmap;            // (ceil(N/32)) unique(idx) bitmap (workspace, zeroed per frame)
+  double* partials;            // (nparts, 40) block partial sums (workspace)
+  TrackState* state;
+};

@@ -1,0 +1,442 @@
+// Dense projective matching for MI355X (gfx950): prep (ray image + gradients), iterative
+// projection (LM over a bilinear ray image), occlusion test and coarse-to-fine descriptor refine.
+//
+// Reference semantics:
+//   prep_for_iter_proj + img_gradient   /root/reference/mast3r_slam/matching.py:25-49, image.py:5-38
+//   iter_proj_kernel                    backend/src/matching_kernels.cu:119-275
+//   occlusion check                     matching.py:68-76
+//   refine_matches_kernel (c10::Half)   backend/src/matching_kernels.cu:25-81
+//   pixel_to_lin                        matching.py:13-15
+//
+// This file is compiled with -ffp-contract=off: the refine score must round every half product and
+// every half add separately (c10::Half operator* / operator+), which a contracted v_fma_f16 breaks.
+#include "m3s_common.hpp"
+
+namespace m3s {
+
+typedef _Float16 h1;
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------------------------------------
+// prep: rays = X/max(|X|,1e-12); gx, gy = Scharr/32 with reflect padding; out (B,H,W,9).
+// One 16x16 tile per 256-thread block, normalised rays of an 18x18 halo staged in LDS.
+// Also converts D11 (B,H,W,F) f32 -> f16 (RNE, == torch .half()) for the same pixels.
+// ------------------------------------------------------------------------------------------
+#define PREP_T 16
+__global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict__ X11, float* __restrict__ rays9,
+                                                        const float* __restrict__ D11, h1* __restrict__ D11h, int H,
+                                                        int W, int F) {
+  __shared__ float tile[(PREP_T + 2) * (PREP_T + 2) * 3];
+  const int b = blockIdx.z;
+  const int u0 = blockIdx.x * PREP_T, v0 = blockIdx.y * PREP_T;
+  const float* Xb = X11 + (size_t)b * H * W * 3;
+  for (int t = threadIdx.x; t < (PREP_T + 2) * (PREP_T + 2); t += blockDim.x) {
+    const int ly = t / (PREP_T + 2), lx = t % (PREP_T + 2);
+    int y = v0 + ly - 1, x = u0 + lx - 1;
+    // reflect padding (F.pad mode="reflect"): -1 -> 1, H -> H-2
+    y = y < 0 ? -y : (y >= H ? 2 * H - 2 - y : y);
+    x = x < 0 ? -x : (x >= W ? 2 * W - 2 - x : x);
+    y = min(max(y, 0), H - 1);
+    x = min(max(x, 0), W - 1);
+    const float* p = Xb + ((size_t)y * W + x) * 3;
+    const float a = p[0], c = p[1], d = p[2];
+    const float n = fmaxf(sqrtf(a * a + c * c + d * d), 1e-12f);
+    tile[t * 3 + 0] = a / n;
+    tile[t * 3 + 1] = c / n;
+    tile[t * 3 + 2] = d / n;
+  }
+  __syncthreads();
+  const int lx = threadIdx.x % PREP_T, ly = threadIdx.x / PREP_T;
+  const int x = u0 + lx, y = v0 + ly;
+  if (x < W && y < H) {
+    float* o = rays9 + (((size_t)b * H + y) * W + x) * 9;
+#define T3(dy, dx, c) tile[(((ly + 1 + (dy)) * (PREP_T + 2)) + (lx + 1 + (dx))) * 3 + (c)]
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      o[c] = T3(0, 0, c);
+      // gx kernel (1/32)[[-3,0,3],[-10,0,10],[-3,0,3]]; gy its transpose (image.py:10-24)
+      const float gx = -0.09375f * T3(-1, -1, c) + 0.09375f * T3(-1, 1, c) - 0.3125f * T3(0, -1, c) +
+                       0.3125f * T3(0, 1, c) - 0.09375f * T3(1, -1, c) + 0.09375f * T3(1, 1, c);
+      const float gy = -0.09375f * T3(-1, -1, c) - 0.3125f * T3(-1, 0, c) - 0.09375f * T3(-1, 1, c) +
+                       0.09375f * T3(1, -1, c) + 0.3125f * T3(1, 0, c) + 0.09375f * T3(1, 1, c);
+      o[3 + c] = gx;
+      o[6 + c] = gy;
+    }
+#undef T3
+  }
+  if (D11 != nullptr) {
+    // f32 -> f16 of this tile's descriptor rows, 4 channels per lane-step
+    for (int t = threadIdx.x; t < PREP_T * PREP_T * (F / 4); t += blockDim.x) {
+      const int pix = t / (F / 4), q = t % (F / 4);
+      const int xx = u0 + pix % PREP_T, yy = v0 + pix / PREP_T;
+      if (xx < W && yy < H) {
+        const size_t off = (((size_t)b * H + yy) * W + xx) * F + q * 4;
+        const float4 v = *reinterpret_cast<const float4*>(D11 + off);
+        h1 r[4] = {(h1)v.x, (h1)v.y, (h1)v.z, (h1)v.w};
+        *reinterpret_cast<uint2*>(D11h + off) = *reinterpret_cast<uint2*>(r);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// iter_proj core (matching_kernels.cu:139-273), one point per lane.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void bilin_w(float u, float v, int& u11, int& v11, float w[4]) {
+  u11 = (int)floorf(u);
+  v11 = (int)floorf(v);
+  const float du = u - (float)u11;
+  const float dv = v - (float)v11;
+  w[0] = du * dv;
+  w[1] = (float)((1.0 - (double)du) * (double)dv);  // (1.0-du)*dv in double (:162)
+  w[2] = (float)((double)du * (1.0 - (double)dv));
+  w[3] = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+}
+
+template <int NC>
+__device__ __forceinline__ void bilin_sample(const float* __restrict__ img, int W, int u11, int v11, const float w[4],
+                                             float* out) {
+  const float* r11 = img + ((size_t)(v11 + 1) * W + (u11 + 1)) * 9;
+  const float* r12 = img + ((size_t)(v11 + 1) * W + u11) * 9;
+  const float* r21 = img + ((size_t)v11 * W + (u11 + 1)) * 9;
+  const float* r22 = img + ((size_t)v11 * W + u11) * 9;
+#pragma unroll
+  for (int j = 0; j < NC; j++) out[j] = w[0] * r11[j] + w[1] * r12[j] + w[2] * r21[j] + w[3] * r22[j];
+}
+
+__device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, int H, int W, const float p[3],
+                                                float& u, float& v, bool& conv, int max_iter, float lambda_init,
+                                                float cost_thresh) {
+  u = fminf(fmaxf(u, 1.0f), (float)(W - 2));
+  v = fminf(fmaxf(v, 1.0f), (float)(H - 2));
+  float lambda = lambda_init;
+  for (int i = 0; i < max_iter; i++) {
+    int u11, v11;
+    float w[4], s[9];
+    bilin_w(u, v, u11, v11, w);
+    bilin_sample<9>(img, W, u11, v11, w, s);
+    // 1.0/r_norm in double then float == IEEE float division (53 >= 2*24+2, innocuous double rounding)
+    float r_norm_inv = 1.0f / sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    const float e0 = s[0] * r_norm_inv - p[0];
+    const float e1 = s[1] * r_norm_inv - p[1];
+    const float e2 = s[2] * r_norm_inv - p[2];
+    const float cost = e0 * e0 + e1 * e1 + e2 * e2;
+    float A00 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
+    const float A01 = s[3] * s[6] + s[4] * s[7] + s[5] * s[8];
+    float A11 = s[6] * s[6] + s[7] * s[7] + s[8] * s[8];
+    const float b0 = -(e0 * s[3] + e1 * s[4] + e2 * s[5]);
+    const float b1 = -(e0 * s[6] + e1 * s[7] + e2 * s[8]);
+    A00 += lambda;
+    A11 += lambda;
+    const float det_inv = 1.0f / (A00 * A11 - A01 * A01);
+    float u_new = u + det_inv * (A11 * b0 - A01 * b1);
+    float v_new = v + det_inv * (-A01 * b0 + A00 * b1);
+    u_new = fminf(fmaxf(u_new, 1.0f), (float)(W - 2));
+    v_new = fminf(fmaxf(v_new, 1.0f), (float)(H - 2));
+    bilin_w(u_new, v_new, u11, v11, w);
+    float r[3];
+    bilin_sample<3>(img, W, u11, v11, w, r);
+    r_norm_inv = 1.0f / sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    const float f0 = r[0] * r_norm_inv - p[0];
+    const float f1 = r[1] * r_norm_inv - p[1];
+    const float f2 = r[2] * r_norm_inv - p[2];
+    const float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
+    if (new_cost < cost) {
+      u = u_new;
+      v = v_new;
+      lambda = (float)((double)lambda * 0.1);
+      conv = new_cost < cost_thresh;
+    } else {
+      lambda = (float)((double)lambda * 10.0);
+      conv = cost < cost_thresh;
+    }
+  }
+}
+
+// Reference-signature kernel: rays (B,H,W,9), pts (B,N,3) normalised, p_init (B,N,2) f32.
+__global__ void __launch_bounds__(256) iter_proj_kernel(const float* __restrict__ rays, const float* __restrict__ pts,
+                                                        const float* __restrict__ p_init, float* __restrict__ p_new,
+                                                        uint8_t* __restrict__ converged, int H, int W, int N,
+                                                        int max_iter, float lambda_init, float cost_thresh) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const size_t bn = (size_t)b * N + n;
+  const float p[3] = {pts[bn * 3 + 0], pts[bn * 3 + 1], pts[bn * 3 + 2]};
+  float u = p_init[bn * 2 + 0], v = p_init[bn * 2 + 1];
+  bool conv = false;
+  iter_proj_point(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh);
+  p_new[bn * 2 + 0] = u;
+  p_new[bn * 2 + 1] = v;
+  converged[bn] = conv;
+}
+
+// Fused: normalise X21 on the fly, p_init from idx_init (or identity), LM projection, .long()
+// truncation, occlusion test against raw X11 (matching.py:68-76). Writes p1 (B,N,2) int32 and
+// valid (B,N) u8.
+__global__ void __launch_bounds__(256) proj_occlusion_kernel(
+    const float* __restrict__ rays, const float* __restrict__ X11, const float* __restrict__ X21,
+    const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
+    int max_iter, float lambda_init, float cost_thresh, float dist_thresh) {
+  const int N = H * W;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const size_t bn = (size_t)b * N + n;
+  const float x = X21[bn * 3 + 0], y = X21[bn * 3 + 1], z = X21[bn * 3 + 2];
+  const float nrm = fmaxf(sqrtf(x * x + y * y + z * z), 1e-12f);
+  const float p[3] = {x / nrm, y / nrm, z / nrm};
+  const int64_t i0 = idx_init != nullptr ? idx_init[bn] : (int64_t)n;
+  // lin_to_pixel (matching.py:18-22) with Python floor semantics for any i0 sign
+  int64_t vq = i0 / W, uq = i0 % W;
+  if (uq < 0) {
+    uq += W;
+    vq -= 1;
+  }
+  float u = (float)uq, v = (float)vq;
+  bool conv = false;
+  iter_proj_point(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh);
+  const int pu = (int)u, pv = (int)v;  // .long() truncation; u,v >= 1 after clamping
+  const float* Xg = X11 + (((size_t)b * H + pv) * W + pu) * 3;
+  const float dx = Xg[0] - x, dy = Xg[1] - y, dz = Xg[2] - z;
+  const float d = sqrtf(dx * dx + dy * dy + dz * dz);
+  p1[bn * 2 + 0] = pu;
+  p1[bn * 2 + 1] = pv;
+  valid[bn] = conv && (d < dist_thresh);
+}
+
+// ------------------------------------------------------------------------------------------
+// refine (matching_kernels.cu:36-80) with c10::Half step rounding: each product and each
+// partial sum rounds to binary16 (v_pk_mul_f16 / v_add_f16 are correctly rounded, == Half ops).
+// ------------------------------------------------------------------------------------------
+template <int F>
+__device__ __forceinline__ h1 score_f16(const h2* q, const h1* __restrict__ c) {
+  h2 cv[F / 2];
+  const uint4* c4 = reinterpret_cast<const uint4*>(c);
+#pragma unroll
+  for (int k = 0; k < F / 8; k++) {
+    const uint4 t = c4[k];
+    cv[4 * k + 0] = *reinterpret_cast<const h2*>(&t.x);
+    cv[4 * k + 1] = *reinterpret_cast<const h2*>(&t.y);
+    cv[4 * k + 2] = *reinterpret_cast<const h2*>(&t.z);
+    cv[4 * k + 3] = *reinterpret_cast<const h2*>(&t.w);
+  }
+  h1 s = (h1)0.0f;
+#pragma unroll
+  for (int k = 0; k < F / 2; k++) {
+    const h2 pr = q[k] * cv[k];
+    s = s + pr.x;
+    s = s + pr.y;
+  }
+  return s;
+}
+
+// D21 row source: f16 (reference signature, caller did .half()) or f32 (fused path: convert here).
+template <int F, bool D21_F32>
+__device__ __forceinline__ void load_query(const void* D21, size_t row, h2* q) {
+  if constexpr (D21_F32) {
+    const float4* s = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(D21) + row * F);
+#pragma unroll
+    for (int k = 0; k < F / 4; k++) {
+      const float4 v = s[k];
+      q[2 * k + 0] = h2{(h1)v.x, (h1)v.y};
+      q[2 * k + 1] = h2{(h1)v.z, (h1)v.w};
+    }
+  } else {
+    const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const h1*>(D21) + row * F);
+#pragma unroll
+    for (int k = 0; k < F / 8; k++) {
+      const uint4 t = s[k];
+      q[4 * k + 0] = *reinterpret_cast<const h2*>(&t.x);
+      q[4 * k + 1] = *reinterpret_cast<const h2*>(&t.y);
+      q[4 * k + 2] = *reinterpret_cast<const h2*>(&t.z);
+      q[4 * k + 3] = *reinterpret_cast<const h2*>(&t.w);
+    }
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void refine_point(const h1* __restrict__ img, int H, int W, const h2* q, int radius,
+                                             int dilation_max, int& u0, int& v0) {
+  h1 max_score = (h1)0.0f;  // cuda::std::numeric_limits<c10::Half>::min() == Half() == +0
+  int u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; d--) {
+    const int rd = radius * d;
+    const int diam = 2 * rd + 1;
+    for (int i = 0; i < diam; i += d) {
+      const int u = u0 - rd + i;
+      for (int j = 0; j < diam; j += d) {
+        const int v = v0 - rd + j;
+        if (v >= 0 && v < H && u >= 0 && u < W) {
+          const h1 s = score_f16<F>(q, img + ((size_t)v * W + u) * F);
+          if (s > max_score) {
+            max_score = s;
+            u_new = u;
+            v_new = v;
+          }
+        }
+      }
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+}
+
+// Reference signature: D11 (B,H,W,F) f16, D21 (B,N,F) f16, p1 (B,N,2) i64 -> p1_new (B,N,2) i64.
+template <int F>
+__global__ void __launch_bounds__(256) refine_f16_kernel(const h1* __restrict__ D11, const h1* __restrict__ D21,
+                                                         const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
+                                                         int H, int W, int N, int radius, int dilation_max) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const size_t bn = (size_t)b * N + n;
+  h2 q[F / 2];
+  load_query<F, false>(D21, bn, q);
+  int u0 = (int)p1[bn * 2 + 0], v0 = (int)p1[bn * 2 + 1];
+  refine_point<F>(D11 + (size_t)b * H * W * F, H, W, q, radius, dilation_max, u0, v0);
+  p1_new[bn * 2 + 0] = u0;
+  p1_new[bn * 2 + 1] = v0;
+}
+
+// Fused tail: D21 f32 converted in-register, p1 int32 from proj_occlusion, writes idx = u + W*v.
+template <int F>
+__global__ void __launch_bounds__(256) refine_lin_kernel(const h1* __restrict__ D11h, const float* __restrict__ D21,
+                                                         const int* __restrict__ p1, int64_t* __restrict__ idx_out,
+                                                         int H, int W, int radius, int dilation_max) {
+  const int N = H * W;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const size_t bn = (size_t)b * N + n;
+  h2 q[F / 2];
+  load_query<F, true>(D21, bn, q);
+  int u0 = p1[bn * 2 + 0], v0 = p1[bn * 2 + 1];
+  refine_point<F>(D11h + (size_t)b * H * W * F, H, W, q, radius, dilation_max, u0, v0);
+  idx_out[bn] = (int64_t)u0 + (int64_t)W * v0;
+}
+
+// fp32 instantiation of the reference kernel (AT_DISPATCH float): fp32 MACs, max starts at FLT_MIN.
+__global__ void __launch_bounds__(256) refine_f32_kernel(const float* __restrict__ D11, const float* __restrict__ D21,
+                                                         const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
+                                                         int H, int W, int F, int N, int radius, int dilation_max) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const size_t bn = (size_t)b * N + n;
+  const float* q = D21 + bn * F;
+  const float* img = D11 + (size_t)b * H * W * F;
+  int u0 = (int)p1[bn * 2 + 0], v0 = (int)p1[bn * 2 + 1];
+  float max_score = 1.17549435e-38f;  // FLT_MIN
+  int u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; d--) {
+    const int rd = radius * d, diam = 2 * rd + 1;
+    for (int i = 0; i < diam; i += d) {
+      for (int j = 0; j < diam; j += d) {
+        const int u = u0 - rd + i, v = v0 - rd + j;
+        if (v >= 0 && v < H && u >= 0 && u < W) {
+          const float* c = img + ((size_t)v * W + u) * F;
+          float s = 0.0f;
+          for (int k = 0; k < F; k++) s += q[k] * c[k];
+          if (s > max_score) {
+            max_score = s;
+            u_new = u;
+            v_new = v;
+          }
+        }
+      }
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  p1_new[bn * 2 + 0] = u0;
+  p1_new[bn * 2 + 1] = v0;
+}
+
+}  // namespace m3s
+
+// ------------------------------------------------------------------------------------------
+// launchers (called from abi.cpp)
+// ------------------------------------------------------------------------------------------
+extern "C" hipError_t m3s_launch_prep(const float* X11, float* rays9, const float* D11, void* D11h, int B, int H,
+                                      int W, int F, hipStream_t s) {
+  dim3 grid((W + PREP_T - 1) / PREP_T, (H + PREP_T - 1) / PREP_T, B);
+  hipLaunchKernelGGL(m3s::prep_rays_kernel, grid, dim3(256), 0, s, X11, rays9, D11,
+                     reinterpret_cast<m3s::h1*>(D11h), H, W, F);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
+                                           uint8_t* conv, int B, int H, int W, int N, int max_iter, float lambda_init,
+                                           float cost_thresh, hipStream_t s) {
+  dim3 grid((N + 255) / 256, B);
+  hipLaunchKernelGGL(m3s::iter_proj_kernel, grid, dim3(256), 0, s, rays, pts, p_init, p_new, conv, H, W, N,
+                     max_iter, lambda_init, cost_thresh);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* X11, const float* X21,
+                                                const int64_t* idx_init, int* p1, uint8_t* valid, int B, int H, int W,
+                                                int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
+                                                hipStream_t s) {
+  dim3 grid((H * W + 255) / 256, B);
+  hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
+                     max_iter, lambda_init, cost_thresh, dist_thresh);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_refine_f16(const void* D11, const void* D21, const int64_t* p1, int64_t* p1_new, int B,
+                                            int H, int W, int F, int N, int radius, int dilation_max, hipStream_t s) {
+  dim3 grid((N + 255) / 256, B);
+  const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11);
+  const m3s::h1* q = reinterpret_cast<const m3s::h1*>(D21);
+  switch (F) {
+    case 24:
+      hipLaunchKernelGGL(m3s::refine_f16_kernel<24>, grid, dim3(256), 0, s, a, q, p1, p1_new, H, W, N, radius,
+                         dilation_max);
+      break;
+    case 16:
+      hipLaunchKernelGGL(m3s::refine_f16_kernel<16>, grid, dim3(256), 0, s, a, q, p1, p1_new, H, W, N, radius,
+                         dilation_max);
+      break;
+    case 32:
+      hipLaunchKernelGGL(m3s::refine_f16_kernel<32>, grid, dim3(256), 0, s, a, q, p1, p1_new, H, W, N, radius,
+                         dilation_max);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_refine_f32(const float* D11, const float* D21, const int64_t* p1, int64_t* p1_new,
+                                            int B, int H, int W, int F, int N, int radius, int dilation_max,
+                                            hipStream_t s) {
+  dim3 grid((N + 255) / 256, B);
+  hipLaunchKernelGGL(m3s::refine_f32_kernel, grid, dim3(256), 0, s, D11, D21, p1, p1_new, H, W, F, N, radius,
+                     dilation_max);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_refine_lin(const void* D11h, const float* D21, const int* p1, int64_t* idx_out, int B,
+                                            int H, int W, int F, int radius, int dilation_max, hipStream_t s) {
+  dim3 grid((H * W + 255) / 256, B);
+  const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
+  switch (F) {
+    case 24:
+      hipLaunchKernelGGL(m3s::refine_lin_kernel<24>, grid, dim3(256), 0, s, a, D21, p1, idx_out, H, W, radius,
+                         dilation_max);
+      break;
+    case 16:
+      hipLaunchKernelGGL(m3s::refine_lin_kernel<16>, grid, dim3(256), 0, s, a, D21, p1, idx_out, H, W, radius,
+                         dilation_max);
+      break;
+    case 32:
+      hipLaunchKernelGGL(m3s::refine_lin_kernel<32>, grid, dim3(256), 0, s, a, D21, p1, idx_out, H, W, radius,
+                         dilation_max);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

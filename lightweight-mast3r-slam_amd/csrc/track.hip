@@ -1,0 +1,412 @@
+// Per-frame tracking Gauss-Newton (Sim(3), pointmap residuals) for MI355X (gfx950).
+//
+// Reference semantics:
+//   FrameTracker.track pre-GN setup    /root/reference/mast3r_slam/tracker.py:35-70, 129-154
+//   FrameTracker.solve                 tracker.py:156-171 (+ nonlinear_optimizer.huber :28-33)
+//   opt_pose_ray_dist_sim3             tracker.py:173-214 (geometry.act_Sim3 :45-52, point_to_ray_dist :17-34)
+//   opt_pose_calib_sim3                tracker.py:216-266 (geometry.project_calib :63-104,
+//                                      constrain_points_to_ray / backproject :37-42, 107-115)
+//   check_convergence                  nonlinear_optimizer.py:5-25
+//   keyframe fusion + selection stats  tracker.py:95-114, frame.py:41-77 (weighted_pointmap)
+//
+// Device pipeline per frame, no host synchronisation inside:
+//   track_setup  : gather Xf[idx], Qk = sqrt(Qff[idx] Qkf), validity masks, per-point GN record,
+//                  counts (valid_opt, valid_kf) and the unique(idx[valid]) bitmap
+//   gn_lin (xI)  : 256-thread blocks, fp64 accumulation of the 28 (H upper) + 7 (g) + 1 (cost) sums
+//   gn_solve (xI): one block: fp64 partial reduction, 7x7 Cholesky, tau, T <- Exp(tau) T,
+//                  convergence test, T_WCf = T_WCk T_CkCf; later launches exit immediately
+//   fuse         : keyframe X <- (C X + C' T_CkCf Xkf) / (C + C'), C += C' when tracking succeeded
+#include "m3s_common.hpp"
+#include "m3s_track.h"
+
+namespace m3s {
+
+#define GN_NSUM 36
+#define GN_PSTRIDE 40
+
+// lietorch group product with the product quaternion re-normalised (RxSO3 ctor), float.
+__device__ __forceinline__ void sim3_mul_norm(const float* A, const float* B, float* C) {
+  float q[4];
+  quat_comp(&A[3], &B[3], q);
+  const float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  float t[3];
+  actSO3(&A[3], &B[0], t);
+  C[0] = A[0] + A[7] * t[0];
+  C[1] = A[1] + A[7] * t[1];
+  C[2] = A[2] + A[7] * t[2];
+  C[3] = q[0] / n;
+  C[4] = q[1] / n;
+  C[5] = q[2] / n;
+  C[6] = q[3] / n;
+  C[7] = A[7] * B[7];
+}
+
+__device__ __forceinline__ void sim3_inv(const float* A, float* C) {
+  const float qi[4] = {-A[3], -A[4], -A[5], A[6]};
+  const float si = 1.0f / A[7];
+  float t[3];
+  actSO3(qi, &A[0], t);
+  C[0] = -si * t[0];
+  C[1] = -si * t[1];
+  C[2] = -si * t[2];
+  C[3] = qi[0];
+  C[4] = qi[1];
+  C[5] = qi[2];
+  C[6] = qi[3];
+  C[7] = si;
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  int v_opt = 0, v_kf = 0;
+  if (n < p.N && p.direct) {  // opt_pose_* surface: Qff = Qk, valid_match = valid, Xf pre-gathered
+    const float qk = a.Qff[n];
+    const bool valid_opt = a.valid_match[n] != 0;
+    v_opt = valid_opt;
+    v_kf = valid_opt;
+    const float sq = valid_opt ? sqrtf(qk) : 0.0f;
+    float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
+    const float* Xf = a.Xf + (size_t)n * 3;
+    if (p.mode == 0) {
+      const float* Xk = a.Xk + (size_t)n * 3;
+      const float d = sqrtf(Xk[0] * Xk[0] + Xk[1] * Xk[1] + Xk[2] * Xk[2]);
+      const float di = 1.0f / d;
+      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
+      rec[1] = make_float4(di * Xk[1], di * Xk[2], d, sq);
+    } else {
+      const float* m = a.meas_k + (size_t)n * 3;
+      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], m[0]);
+      rec[1] = make_float4(m[1], m[2], a.valid_meas[n] ? 1.0f : 0.0f, sq);
+    }
+  } else if (n < p.N) {
+    const int64_t i = a.idx[n];
+    const float qk = sqrtf(a.Qff[i] * a.Qkf[n]);
+    const float cf = a.Cf[i] / p.Nf;  // frame.get_average_conf(): C / N
+    const float ck = a.Ck[n] / p.Nk;
+    const bool vm = a.valid_match[n] != 0;
+    const bool valid_opt = vm && (cf > p.C_conf) && (ck > p.C_conf) && (qk > p.Q_conf);
+    v_opt = valid_opt;
+    v_kf = vm && (qk > p.Q_conf);
+    if (vm) atomicOr(&a.bitmap[i >> 5], 1u << (i & 31));
+    const float sq = valid_opt ? sqrtf(qk) : 0.0f;
+    float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
+    const float* Xf = a.Xf + i * 3;
+    const float* Xk = a.Xk + (size_t)n * 3;
+    if (p.mode == 0) {  // rays: [Xf[idx], rd_k = (Xk/|Xk|, |Xk|), sqrtQ*valid]
+      const float d = sqrtf(Xk[0] * Xk[0] + Xk[1] * Xk[1] + Xk[2] * Xk[2]);
+      const float di = 1.0f / d;
+      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
+      rec[1] = make_float4(di * Xk[1], di * Xk[2], d, sq);
+    } else {  // calib: constrain_points_to_ray at pixel idx, meas_k = [u_n, v_n, log z_k]
+      const float uf = (float)(i % p.W), vf = (float)(i / p.W);
+      const float zf = Xf[2];
+      const float xc = zf * ((uf - p.cx) / p.fx);
+      const float yc = zf * ((vf - p.cy) / p.fy);
+      const float zk = Xk[2];
+      const bool vmeas = zk > p.depth_eps;
+      const float un = (float)(n % p.W), vn = (float)(n / p.W);
+      rec[0] = make_float4(xc, yc, zf, vmeas ? un : 0.0f);
+      rec[1] = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
+    }
+  }
+  // block-reduce the two counters, one atomic per block
+  __shared__ int s_cnt[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long bo = __ballot(v_opt), bk = __ballot(v_kf);
+  if (lane == 0) {
+    s_cnt[0][wid] = __popcll(bo);
+    s_cnt[1][wid] = __popcll(bk);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&a.state->n_valid_opt, s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3]);
+    atomicAdd(&a.state->n_valid_kf, s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3]);
+  }
+}
+
+__device__ __forceinline__ bool track_skipped(const TrackState* st, const TrackParams& p) {
+  return (float)st->n_valid_opt / (float)p.N < p.min_match_frac;  // tracker.py:67-70
+}
+
+// accumulate one whitened row (tracker.py:156-166): robust = si*sqrt(huber(si*r)); A = robust*J; b = robust*r
+__device__ __forceinline__ void acc_row(double* acc, const float J[7], float r, float si, float k) {
+  const float wr = si * r;
+  const float ra = fabsf(wr);
+  const float hub = ra < k ? 1.0f : k / ra;
+  const float rob = si * sqrtf(hub);
+  float A[7];
+#pragma unroll
+  for (int c = 0; c < 7; c++) A[c] = rob * J[c];
+  const float b = rob * r;
+  int l = 0;
+#pragma unroll
+  for (int c = 0; c < 7; c++) {
+#pragma unroll
+    for (int d = c; d < 7; d++) acc[l++] += (double)A[c] * (double)A[d];
+  }
+#pragma unroll
+  for (int c = 0; c < 7; c++) acc[28 + c] -= (double)A[c] * (double)b;  // g = -A^T b
+  acc[35] += 0.5 * (double)b * (double)b;
+}
+
+// J = -(d h / d Y) [I, -[Y]x, Y]; dh is a 3-vector row of the measurement Jacobian
+__device__ __forceinline__ void chain_row(const float dh[3], const float Y[3], float J[7]) {
+  // S = -skew(Y) = [[0, z, -y], [-z, 0, x], [y, -x, 0]] (geometry.act_Sim3 dpC_dR)
+  J[0] = -dh[0];
+  J[1] = -dh[1];
+  J[2] = -dh[2];
+  J[3] = -(dh[1] * -Y[2] + dh[2] * Y[1]);
+  J[4] = -(dh[0] * Y[2] + dh[2] * -Y[0]);
+  J[5] = -(dh[0] * -Y[1] + dh[1] * Y[0]);
+  J[6] = -(dh[0] * Y[0] + dh[1] * Y[1] + dh[2] * Y[2]);
+}
+
+__global__ void __launch_bounds__(256) gn_lin_kernel(TrackArgs a, TrackParams p) {
+  const TrackState* st = a.state;
+  if (st->done || track_skipped(st, p)) return;
+  float T[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) T[c] = st->T[c];
+  double acc[GN_NSUM];
+#pragma unroll
+  for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
+  const float4* rec = reinterpret_cast<const float4*>(a.rec);
+  const int stride = gridDim.x * blockDim.x;
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < p.N; n += stride) {
+    const float4 r0 = rec[2 * (size_t)n], r1 = rec[2 * (size_t)n + 1];
+    const float X[3] = {r0.x, r0.y, r0.z};
+    float Y[3];
+    actSim3(T, X, Y);
+    const float sq = r1.w;
+    if (p.mode == 0) {
+      const float d = sqrtf(Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2]);
+      const float di = 1.0f / d;
+      const float di2 = di * di;
+      const float rr[3] = {di * Y[0], di * Y[1], di * Y[2]};
+      const float res[4] = {r0.w - rr[0], r1.x - rr[1], r1.y - rr[2], r1.z - d};
+      const float si_r = p.c_a * sq, si_d = p.c_b * sq;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        float dh[3];
+#pragma unroll
+        for (int m = 0; m < 3; m++) dh[m] = di * ((k == m ? 1.0f : 0.0f) - di2 * (Y[k] * Y[m]));
+        float J[7];
+        chain_row(dh, Y, J);
+        acc_row(acc, J, res[k], si_r, p.huber_k);
+      }
+      float J[7];
+      chain_row(rr, Y, J);
+      acc_row(acc, J, res[3], si_d, p.huber_k);
+    } else {
+      const float x = Y[0], y = Y[1], z = Y[2];
+      const float pu = p.K[0] * x + p.K[1] * y + p.K[2] * z;
+      const float pv = p.K[3] * x + p.K[4] * y + p.K[5] * z;
+      const float pw = p.K[6] * x + p.K[7] * y + p.K[8] * z;
+      const float u = pu / pw, v = pv / pw;
+      const bool valid_z = z > p.depth_eps;
+      const float logz = valid_z ? logf(z) : 0.0f;
+      const bool valid = (u > p.pixel_border) && (u < (float)(p.W - 1) - p.pixel_border) &&
+                         (v > p.pixel_border) && (v < (float)(p.H - 1) - p.pixel_border) && valid_z &&
+                         (r1.z != 0.0f);
+      const float vf = valid ? 1.0f : 0.0f;
+      const float si_p = vf * (p.c_a * sq), si_z = vf * (p.c_b * sq);
+      const float zi = 1.0f / z;
+      const float res[3] = {r0.w - u, r1.x - v, r1.y - logz};
+      float dh[3], J[7];
+      dh[0] = p.K[0] * zi;
+      dh[1] = 0.0f;
+      dh[2] = (-p.K[0] * x * zi) * zi;
+      chain_row(dh, Y, J);
+      acc_row(acc, J, res[0], si_p, p.huber_k);
+      dh[0] = 0.0f;
+      dh[1] = p.K[4] * zi;
+      dh[2] = (-p.K[4] * y * zi) * zi;
+      chain_row(dh, Y, J);
+      acc_row(acc, J, res[1], si_p, p.huber_k);
+      dh[0] = 0.0f;
+      dh[1] = 0.0f;
+      dh[2] = zi;
+      chain_row(dh, Y, J);
+      acc_row(acc, J, res[2], si_z, p.huber_k);
+    }
+  }
+  // wave64 butterfly, then the 4 waves through LDS; fp64 throughout
+  __shared__ double s_part[4][GN_NSUM];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < GN_NSUM; c++) {
+    const double v = wave_sum(acc[c]);
+    if (lane == 0) s_part[wid][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < GN_NSUM) {
+    const int c = threadIdx.x;
+    a.partials[(size_t)blockIdx.x * GN_PSTRIDE + c] = s_part[0][c] + s_part[1][c] + s_part[2][c] + s_part[3][c];
+  }
+}
+
+// 7x7 fp64 Cholesky solve H tau = g; false when H is not positive definite (torch.linalg.cholesky raises)
+__device__ bool chol7(double H[7][7], double g[7], double tau[7]) {
+  double L[7][7];
+  for (int j = 0; j < 7; j++) {
+    double d = H[j][j];
+    for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
+    if (!(d > 0.0)) return false;
+    d = sqrt(d);
+    L[j][j] = d;
+    for (int i = j + 1; i < 7; i++) {
+      double s = H[i][j];
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+      L[i][j] = s / d;
+    }
+  }
+  double y[7];
+  for (int i = 0; i < 7; i++) {
+    double s = g[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 6; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < 7; k++) s -= L[k][i] * tau[k];
+    tau[i] = s / L[i][i];
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) gn_solve_kernel(TrackArgs a, TrackParams p, int nparts) {
+  TrackState* st = a.state;
+  __shared__ double s_sum[GN_NSUM];
+  __shared__ int s_bits[4];
+  if (st->iter == 0 && st->n_unique < 0) {  // unique(idx[valid_match]) count, once per frame
+    int cnt = 0;
+    for (int w = threadIdx.x; w < (p.N + 31) / 32; w += blockDim.x) cnt += __popc(a.bitmap[w]);
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if ((threadIdx.x & 63) == 0) s_bits[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) st->n_unique = s_bits[0] + s_bits[1] + s_bits[2] + s_bits[3];
+  }
+  if (st->done) return;
+  if (track_skipped(st, p)) {
+    if (threadIdx.x == 0) {
+      st->status = M3S_TRACK_SKIPPED;
+      st->done = 1;
+    }
+    return;
+  }
+  // column-parallel fp64 reduction of the block partials: wave w owns columns w, w+4, ...
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int c = wid; c < GN_NSUM; c += 4) {
+    double v = 0.0;
+    for (int r = lane; r < nparts; r += 64) v += a.partials[(size_t)r * GN_PSTRIDE + c];
+    v = wave_sum(v);
+    if (lane == 0) s_sum[c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double H[7][7], g[7], tau[7];
+  int l = 0;
+  for (int c = 0; c < 7; c++)
+    for (int d = c; d < 7; d++) {
+      H[c][d] = s_sum[l];
+      H[d][c] = s_sum[l];
+      l++;
+    }
+  for (int c = 0; c < 7; c++) g[c] = s_sum[28 + c];
+  const double cost = s_sum[35];
+  st->last_cost = cost;
+  if (!chol7(H, g, tau)) {
+    st->status = M3S_TRACK_CHOLESKY_FAILED;
+    st->done = 1;
+    return;
+  }
+  float tf[7];
+  float tn2 = 0.0f;
+  for (int c = 0; c < 7; c++) {
+    tf[c] = (float)tau[c];
+    tn2 += tf[c] * tf[c];
+  }
+  float E[8], Tn[8];
+  expSim3(tf, E);
+  sim3_mul_norm(E, st->T, Tn);  // T_CkCf.retr(tau) = Exp(tau) * T_CkCf
+  for (int c = 0; c < 8; c++) st->T[c] = Tn[c];
+  const int it = st->iter + 1;
+  st->iter = it;
+  const double old = st->old_cost;
+  const double rel = fabs((old - cost) / old);  // inf/inf = nan on the first step -> false
+  const bool conv = (rel < (double)p.rel_error) || (sqrtf(tn2) < p.delta_norm);
+  st->old_cost = cost;
+  if (conv || it >= p.max_iters) {
+    st->status = conv ? M3S_TRACK_OK : M3S_TRACK_MAX_ITERS;
+    st->done = 1;
+  }
+  if (st->done) sim3_mul_norm(st->T_WCk, st->T, st->T_WCf);  // T_WCf = T_WCk * T_CkCf
+}
+
+// keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77), only when
+// tracking succeeded; X_kf, C_kf updated in place.
+__global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, float* __restrict__ Xkf_canon,
+                                                   float* __restrict__ Ckf_sum, const float* __restrict__ Xkf,
+                                                   const float* __restrict__ Ckf, int N) {
+  if (!(st->done && (st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS))) return;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float T[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) T[c] = st->T[c];
+  const float X[3] = {Xkf[3 * (size_t)n], Xkf[3 * (size_t)n + 1], Xkf[3 * (size_t)n + 2]};
+  float Y[3];
+  actSim3(T, X, Y);
+  const float c0 = Ckf_sum[n], c1 = Ckf[n];
+  const float den = c0 + c1;
+#pragma unroll
+  for (int k = 0; k < 3; k++) Xkf_canon[3 * (size_t)n + k] = (c0 * Xkf_canon[3 * (size_t)n + k] + c1 * Y[k]) / den;
+  Ckf_sum[n] = den;
+}
+
+}  // namespace m3s
+
+namespace m3s {
+// state <- {T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf, n_unique = -1}
+__global__ void track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk) {
+  if (threadIdx.x != 0) return;
+  float Ti[8], Tf[8], Tk[8];
+  for (int c = 0; c < 8; c++) {
+    Tf[c] = T_WCf[c];
+    Tk[c] = T_WCk[c];
+    st->T_WCk[c] = Tk[c];
+  }
+  sim3_inv(Tk, Ti);
+  sim3_mul_norm(Ti, Tf, st->T);
+  st->old_cost = __builtin_inf();
+  st->n_unique = -1;
+}
+}  // namespace m3s
+
+extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_WCf, const float* T_WCk,
+                                            hipStream_t s) {
+  hipLaunchKernelGGL(m3s::track_init_kernel, dim3(1), dim3(64), 0, s, a->state, T_WCf, T_WCk);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_track_setup(const TrackArgs* a, const TrackParams* p, hipStream_t s) {
+  hipLaunchKernelGGL(m3s::track_setup_kernel, dim3((p->N + 255) / 256), dim3(256), 0, s, *a, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackParams* p, int nparts, int iters,
+                                             hipStream_t s) {
+  for (int i = 0; i < iters; i++) {
+    hipLaunchKernelGGL(m3s::gn_lin_kernel, dim3(nparts), dim3(256), 0, s, *a, *p);
+    hipLaunchKernelGGL(m3s::gn_solve_kernel, dim3(1), dim3(256), 0, s, *a, *p, nparts);
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_fuse(const void* state, float* Xkf_canon, float* Ckf_sum, const float* Xkf,
+                                      const float* Ckf, int N, hipStream_t s) {
+  hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s,
+                     reinterpret_cast<const TrackState*>(state), Xkf_canon, Ckf_sum, Xkf, Ckf, N);
+  return hipGetLastError();
+}

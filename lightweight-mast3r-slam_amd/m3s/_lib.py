@@ -1,0 +1,136 @@
+"""ctypes binding of libm3s.so (the C ABI declared in include/m3s.h).
+
+The product path has no fallback: if the HIP library or a GPU is missing, every operator raises
+RuntimeError. Tensors are passed as raw device pointers together with torch's current HIP stream,
+so the kernels are ordered with the caller's other torch work exactly like the reference's
+extension ops (which, unlike these, always used the legacy default stream).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libm3s.so")
+
+c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
+
+
+class BaConfig(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("sigma_a", c_float), ("sigma_b", c_float), ("C_thresh", c_float),
+                ("Q_thresh", c_float), ("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float),
+                ("height", c_int), ("width", c_int), ("pixel_border", c_int), ("z_eps", c_float)]
+
+
+class BaPlan(ctypes.Structure):
+    _fields_ = [("opaque", ctypes.c_ubyte * 768)]
+
+
+class TrackConfig(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("max_iters", c_int), ("C_conf", c_float), ("Q_conf", c_float),
+                ("min_match_frac", c_float), ("sigma_a", c_float), ("sigma_b", c_float), ("huber_k", c_float),
+                ("rel_error", c_float), ("delta_norm", c_float), ("pixel_border", c_float),
+                ("depth_eps", c_float), ("K", c_float * 9), ("H", c_int), ("W", c_int)]
+
+
+class TrackInputs(ctypes.Structure):
+    _fields_ = [("idx_f2k", c_void_p), ("valid_match", c_void_p), ("Xf", c_void_p), ("Cf", c_void_p),
+                ("Nf", c_float), ("Qff", c_void_p), ("Xk", c_void_p), ("Ck", c_void_p), ("Nk", c_float),
+                ("Qkf", c_void_p), ("T_WCf", c_void_p), ("T_WCk", c_void_p), ("direct", c_int),
+                ("meas_k", c_void_p), ("valid_meas_k", c_void_p)]
+
+
+class TrackFuse(ctypes.Structure):
+    _fields_ = [("Xk_canon", c_void_p), ("Ck_sum", c_void_p), ("Xkf", c_void_p), ("Ckf", c_void_p)]
+
+
+class TrackResult(ctypes.Structure):
+    _fields_ = [("T_WCf", c_float * 8), ("T_CkCf", c_float * 8), ("cost", c_double), ("iters", c_int),
+                ("status", c_int), ("n_valid_opt", c_int), ("n_valid_kf", c_int), ("n_unique", c_int),
+                ("N", c_int)]
+
+
+TRACK_OK, TRACK_MAX_ITERS, TRACK_CHOLESKY_FAILED, TRACK_SKIPPED = 1, 2, 3, 4
+
+# exported entry points and their argtypes (restype int unless noted)
+_SIGS = {
+    "m3s_abi_version": ([], c_int),
+    "m3s_last_error": ([], ctypes.c_char_p),
+    "m3s_timing_enable": ([c_int], None),
+    "m3s_timing_reset": ([], None),
+    "m3s_timing_query": ([ctypes.c_char_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int)], c_int),
+    "m3s_iter_proj": ([c_void_p] * 5 + [c_int] * 6 + [c_float, c_float, c_void_p], c_int),
+    "m3s_refine_matches": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
+    "m3s_ba_workspace_size": ([c_int, c_int, c_int], c_size_t),
+    "m3s_gauss_newton": ([ctypes.POINTER(BaConfig), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p,
+                          ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p], c_int),
+    "m3s_ba_make_plan": ([ctypes.POINTER(BaConfig), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                          c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                          c_void_p, c_size_t, ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_edge_sums": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)], c_int),
+    "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_iterations": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), c_void_p], c_int),
+    "m3s_match_workspace_size": ([c_int] * 4, c_size_t),
+    "m3s_match": ([c_void_p] * 7 + [c_int] * 5 + [c_float] * 3 + [c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
+    "m3s_track_workspace_size": ([c_int], c_size_t),
+    "m3s_track": ([ctypes.POINTER(TrackInputs), ctypes.POINTER(TrackConfig), ctypes.POINTER(TrackFuse), c_int,
+                   c_void_p, ctypes.POINTER(TrackResult), c_void_p, c_size_t, c_void_p], c_int),
+}
+
+EXPORTED = sorted(_SIGS)
+
+_LIB = None
+
+
+def load(require_gpu=True):
+    """Load libm3s.so. With require_gpu, raise unless a HIP device is visible to torch."""
+    global _LIB
+    if require_gpu and not torch.cuda.is_available():
+        raise RuntimeError("m3s: no HIP device visible; the MI355X kernels have no CPU fallback")
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"m3s: {LIB_PATH} not built (run __graft_entry__.build() or make -C csrc)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        if lib.m3s_abi_version() != 1:
+            raise RuntimeError("m3s: ABI version mismatch")
+        _LIB = lib
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        msg = _LIB.m3s_last_error().decode() if _LIB is not None else ""
+        raise RuntimeError(f"m3s error {rc}: {msg}")
+
+
+def stream_ptr(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)
+
+
+_WS = {}
+
+
+def workspace(key, nbytes, device):
+    """A cached uint8 device buffer per (key, device), grown on demand (torch caching allocator)."""
+    k = (key, str(device))
+    buf = _WS.get(k)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _WS[k] = buf
+    return buf
+
+
+def require_cuda(name, *tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(f"{name}: tensors must be on the HIP device (got {t.device})")

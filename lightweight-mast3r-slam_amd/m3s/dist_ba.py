@@ -1,0 +1,109 @@
+"""Edge-sharded global BA across GPUs (one process per GPU, RCCL over xGMI).
+
+No reference counterpart: the reference runs BA in one process with a CPU Eigen solve
+(``gn_kernels.cu:1181-1225``). Here:
+
+* the E directed edges are split into contiguous, equal shards (every edge carries the same N
+  points, so equal edge counts are equal work);
+* each rank linearises only its shard into its rows of the (E, 36) fp64 edge-sum table
+  (``M = A L A^T`` upper 28 + ``g = A v`` 7 per edge) — ~0.56 MB at E = 2000;
+* ONE all-reduce(sum) of that table per GN iteration is the only exchange;
+* every rank then assembles the identical block-sparse system in a fixed order, factorises it and
+  retracts the poses, so poses stay bit-identical across ranks without a broadcast.
+
+The backend is pluggable so the protocol itself can be exercised on CPU with ``gloo`` (tests use
+an oracle backend); the product backend is ``HipShard`` over ``libm3s.so``.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from m3s import _lib
+
+BA_MODES = {"points": 0, "rays": 1, "calib": 2}
+
+
+def shard_range(E, rank, world):
+    """Contiguous balanced split of E edges: the first E % world ranks get one extra edge."""
+    q, r = divmod(E, world)
+    e0 = rank * q + min(rank, r)
+    return e0, e0 + q + (1 if rank < r else 0)
+
+
+def ba_config(mode, cfg, K=None, height=0, width=0):
+    m = BA_MODES[mode]
+    c = _lib.BaConfig(mode=m, C_thresh=float(cfg["C_conf"]), Q_thresh=float(cfg["Q_conf"]))
+    if m == 0:
+        c.sigma_a = float(cfg["sigma_point"])
+    elif m == 1:
+        c.sigma_a, c.sigma_b = float(cfg["sigma_ray"]), float(cfg["sigma_dist"])
+    else:
+        Kh = K.detach().float().cpu()
+        c.sigma_a, c.sigma_b = float(cfg["sigma_pixel"]), float(cfg["sigma_depth"])
+        c.fx, c.fy, c.cx, c.cy = float(Kh[0, 0]), float(Kh[1, 1]), float(Kh[0, 2]), float(Kh[1, 2])
+        c.height, c.width = int(height), int(width)
+        c.pixel_border, c.z_eps = int(cfg["pixel_border"]), float(cfg["depth_eps"])
+    return c
+
+
+class HipShard:
+    """One rank's view of a sharded BA problem on its GPU (libm3s split API)."""
+
+    def __init__(self, cfg_struct, Twc, Xs, Cs, ii, jj, idx, valid, Q, delta_thresh, e0, e1):
+        lib = _lib.load()
+        self.lib = lib
+        self.dev = Twc.device
+        Kp, N = Xs.shape[0], Xs.shape[1]
+        E = ii.shape[0]
+        self.Kp, self.E = Kp, E
+        self.dx = torch.zeros((max(Kp - 1, 0), 7), dtype=torch.float32, device=self.dev)
+        nbytes = lib.m3s_ba_workspace_size(Kp, N, E)
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        self.keep = (Twc, Xs, Cs, ii, jj, idx, valid, Q)
+        self.plan = _lib.BaPlan()
+        self.cfg = cfg_struct
+        _lib.check(lib.m3s_ba_make_plan(ctypes.byref(cfg_struct), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs), Kp, N,
+                                        _lib.ptr(ii), _lib.ptr(jj), E, int(e0), int(e1), _lib.ptr(idx),
+                                        _lib.ptr(valid), _lib.ptr(Q), float(delta_thresh), _lib.ptr(self.dx),
+                                        _lib.ptr(self.ws), self.ws.numel(), ctypes.byref(self.plan),
+                                        _lib.stream_ptr(self.dev)))
+        off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
+        _lib.check(lib.m3s_ba_edge_sums(ctypes.byref(self.plan), ctypes.byref(off), ctypes.byref(cnt)))
+        self.edge_sums = self.ws[off.value: off.value + cnt.value].view(torch.float64)
+
+    def linearize(self):
+        _lib.check(self.lib.m3s_ba_linearize(ctypes.byref(self.plan), _lib.stream_ptr(self.dev)))
+
+    def solve(self):
+        _lib.check(self.lib.m3s_ba_solve(ctypes.byref(self.plan), _lib.stream_ptr(self.dev)))
+
+    def iterations(self):
+        it = ctypes.c_int()
+        _lib.check(self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev)))
+        return it.value
+
+
+def run_sharded(shard, max_iter, group=None):
+    """GN loop of one rank: linearise shard -> all-reduce edge sums -> identical solve/retract."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    for _ in range(int(max_iter)):
+        shard.linearize()
+        if world > 1:
+            dist.all_reduce(shard.edge_sums, op=dist.ReduceOp.SUM, group=group)
+        shard.solve()
+    return shard
+
+
+def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter, delta_thresh, K=None, height=0,
+                         width=0, group=None):
+    """Multi-GPU drop-in for mast3r_slam_backends.gauss_newton_*: same inputs (every rank holds the
+    full problem, replicated), Twc updated in place identically on every rank; returns [dx]."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    e0, e1 = shard_range(ii.shape[0], rank, world)
+    c = lambda t: t.contiguous()
+    shard = HipShard(ba_config(mode, cfg, K, height, width), c(Twc), c(Xs), c(Cs.reshape(Xs.shape[0], -1)), c(ii),
+                     c(jj), c(idx), c(valid.reshape(idx.shape)), c(Q.reshape(idx.shape)), delta_thresh, e0, e1)
+    run_sharded(shard, max_iter, group)
+    return [shard.dx]

@@ -1,0 +1,144 @@
+"""``FactorGraph`` with the reference surface (``/root/reference/mast3r_slam/global_opt.py:14-226``).
+
+Edge insertion (``add_factors``) batches the symmetric matches of all new edges through the fused
+HIP matcher; ``solve_GN_rays`` / ``solve_GN_calib`` call the drop-in ``mast3r_slam_backends``
+operators (single GPU) or, when ``torch.distributed`` is initialised with more than one rank, the
+edge-sharded RCCL solve of ``m3s.dist_ba`` (identical result on every rank).
+"""
+import torch
+import torch.distributed as dist
+
+import mast3r_slam_backends
+from m3s.config import config
+from m3s.geometry import constrain_points_to_ray
+from m3s.matching import match
+from m3s.sim3 import Sim3
+
+
+def mast3r_match_symmetric(model, kfs_i, kfs_j):
+    """mast3r_utils.py:149-187 with the ViT decode behind ``model.symmetric_inference`` returning
+    X (4,b,H,W,3), C (4,b,H,W), D (4,b,H,W,F), Q (4,b,H,W) ordered ii, ji, jj, ij."""
+    X, C, D, Q = model.symmetric_inference(kfs_i, kfs_j)
+    b = X.shape[1]
+    X11 = torch.cat((X[0], X[2]), dim=0)
+    X21 = torch.cat((X[1], X[3]), dim=0)
+    D11 = torch.cat((D[0], D[2]), dim=0)
+    D21 = torch.cat((D[1], D[3]), dim=0)
+    idx_1_to_2, valid_match_2 = match(X11, X21, D11, D21)
+    return (idx_1_to_2[:b], idx_1_to_2[b:], valid_match_2[:b], valid_match_2[b:],
+            Q[0].reshape(b, -1, 1), Q[2].reshape(b, -1, 1), Q[1].reshape(b, -1, 1), Q[3].reshape(b, -1, 1))
+
+
+class FactorGraph:
+    def __init__(self, model, frames, K=None, device="cuda"):
+        self.model = model
+        self.frames = frames
+        self.device = device
+        self.cfg = config["local_opt"]
+        e = lambda dt: torch.as_tensor([], dtype=dt, device=device)
+        self.ii, self.jj = e(torch.long), e(torch.long)
+        self.idx_ii2jj, self.idx_jj2ii = e(torch.long), e(torch.long)
+        self.valid_match_j, self.valid_match_i = e(torch.bool), e(torch.bool)
+        self.Q_ii2jj, self.Q_jj2ii = e(torch.float32), e(torch.float32)
+        self.window_size = self.cfg["window_size"]
+        self.K = K
+        self.group = None  # torch.distributed group for the sharded solve (None = WORLD)
+
+    def add_factors(self, ii, jj, min_match_frac, is_reloc=False):
+        """global_opt.py:32-101."""
+        kf_ii = [self.frames[i] for i in ii]
+        kf_jj = [self.frames[j] for j in jj]
+        idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij = mast3r_match_symmetric(
+            self.model, kf_ii, kf_jj)
+        bi = torch.arange(idx_i2j.shape[0], device=idx_i2j.device)[:, None].repeat(1, idx_i2j.shape[1])
+        Qj = torch.sqrt(Qii[bi, idx_i2j] * Qji)
+        Qi = torch.sqrt(Qjj[bi, idx_j2i] * Qij)
+        valid_j = valid_match_j & (Qj > self.cfg["Q_conf"])
+        valid_i = valid_match_i & (Qi > self.cfg["Q_conf"])
+        match_frac_j = valid_j.sum(dim=(1, 2)) / (valid_j.shape[1] * valid_j.shape[2])
+        match_frac_i = valid_i.sum(dim=(1, 2)) / (valid_i.shape[1] * valid_i.shape[2])
+        ii_t = torch.as_tensor(ii, device=self.device)
+        jj_t = torch.as_tensor(jj, device=self.device)
+        invalid = torch.minimum(match_frac_j, match_frac_i) < min_match_frac
+        invalid = (~(ii_t == (jj_t - 1))) & invalid  # consecutive edges are always kept
+        if invalid.any() and is_reloc:
+            return False
+        keep = ~invalid
+        self.ii = torch.cat([self.ii, ii_t[keep]])
+        self.jj = torch.cat([self.jj, jj_t[keep]])
+        self.idx_ii2jj = torch.cat([self.idx_ii2jj, idx_i2j[keep]])
+        self.idx_jj2ii = torch.cat([self.idx_jj2ii, idx_j2i[keep]])
+        self.valid_match_j = torch.cat([self.valid_match_j, valid_match_j[keep]])
+        self.valid_match_i = torch.cat([self.valid_match_i, valid_match_i[keep]])
+        self.Q_ii2jj = torch.cat([self.Q_ii2jj, Qj[keep]])
+        self.Q_jj2ii = torch.cat([self.Q_jj2ii, Qi[keep]])
+        return keep.sum() > 0
+
+    def get_unique_kf_idx(self):
+        return torch.unique(torch.cat([self.ii, self.jj]), sorted=True)
+
+    def prep_two_way_edges(self):
+        ii = torch.cat((self.ii, self.jj), dim=0)
+        jj = torch.cat((self.jj, self.ii), dim=0)
+        idx_ii2jj = torch.cat((self.idx_ii2jj, self.idx_jj2ii), dim=0)
+        valid_match = torch.cat((self.valid_match_j, self.valid_match_i), dim=0)
+        Q_ii2jj = torch.cat((self.Q_ii2jj, self.Q_jj2ii), dim=0)
+        return ii, jj, idx_ii2jj, valid_match, Q_ii2jj
+
+    def get_poses_points(self, unique_kf_idx):
+        kfs = [self.frames[int(i)] for i in unique_kf_idx]
+        Xs = torch.stack([kf.X_canon for kf in kfs])
+        T_WCs = Sim3(torch.stack([kf.T_WC.data.reshape(1, 8) for kf in kfs]))
+        Cs = torch.stack([kf.get_average_conf() for kf in kfs])
+        return Xs, T_WCs, Cs
+
+    def _sharded(self):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def solve_GN_rays(self):
+        """global_opt.py:123-161."""
+        cfg = self.cfg
+        pin = cfg["pin"]
+        unique_kf_idx = self.get_unique_kf_idx()
+        if unique_kf_idx.numel() <= pin:
+            return
+        Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
+        ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
+        pose_data = T_WCs.data[:, 0, :]
+        if self._sharded():
+            from m3s.dist_ba import gauss_newton_sharded
+
+            gauss_newton_sharded("rays", pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj, cfg,
+                                 cfg["max_iters"], cfg["delta_norm"], group=self.group)
+        else:
+            mast3r_slam_backends.gauss_newton_rays(pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
+                                                   cfg["sigma_ray"], cfg["sigma_dist"], cfg["C_conf"], cfg["Q_conf"],
+                                                   cfg["max_iters"], cfg["delta_norm"])
+        self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])
+
+    def solve_GN_calib(self):
+        """global_opt.py:163-226."""
+        cfg = self.cfg
+        K = self.K
+        pin = cfg["pin"]
+        unique_kf_idx = self.get_unique_kf_idx()
+        if unique_kf_idx.numel() <= pin:
+            return
+        Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
+        img_size = self.frames[0].img_size
+        Xs = constrain_points_to_ray(img_size, Xs, K)
+        ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
+        pose_data = T_WCs.data[:, 0, :]
+        height, width = img_size
+        if self._sharded():
+            from m3s.dist_ba import gauss_newton_sharded
+
+            gauss_newton_sharded("calib", pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj, cfg,
+                                 cfg["max_iters"], cfg["delta_norm"], K=K, height=height, width=width,
+                                 group=self.group)
+        else:
+            mast3r_slam_backends.gauss_newton_calib(pose_data, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
+                                                    height, width, cfg["pixel_border"], cfg["depth_eps"],
+                                                    cfg["sigma_pixel"], cfg["sigma_depth"], cfg["C_conf"],
+                                                    cfg["Q_conf"], cfg["max_iters"], cfg["delta_norm"])
+        self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])

@@ -1,0 +1,53 @@
+"""Dense matching: the reference's ``mast3r_slam/matching.py`` surface over fused HIP kernels.
+
+``match`` / ``match_iterative_proj`` keep the reference signatures and return values
+(``matching.py:8-90``): ``idx_1_to_2`` (B, H*W) int64 and ``valid_match2`` (B, H*W, 1) bool. The
+whole function is one C-ABI call (``m3s_match``): ray-image prep + iterative projection + occlusion
+test + half-precision descriptor refine + linear index, three kernels, no host sync.
+"""
+import torch
+
+from m3s import _lib
+from m3s.config import config
+
+
+def pixel_to_lin(p1, w):
+    return p1[..., 0] + (w * p1[..., 1])  # matching.py:13-15
+
+
+def lin_to_pixel(idx_1_to_2, w):
+    u = idx_1_to_2 % w  # matching.py:18-22
+    v = idx_1_to_2 // w
+    return torch.stack((u, v), dim=-1)
+
+
+def match(X11, X21, D11, D21, idx_1_to_2_init=None):
+    return match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init)
+
+
+def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None):
+    cfg = config["matching"]
+    lib = _lib.load()
+    _lib.require_cuda("match", X11, X21, D11, D21, idx_1_to_2_init)
+    b, h, w = X21.shape[:3]
+    F = D11.shape[-1]
+    X11 = X11.float().contiguous()
+    X21 = X21.float().contiguous()
+    D11 = D11.float().contiguous()
+    D21 = D21.float().reshape(b, h, w, F).contiguous()
+    if tuple(X11.shape) != (b, h, w, 3) or tuple(D11.shape) != (b, h, w, F):
+        raise RuntimeError("match: X11/X21 (B,H,W,3) and D11/D21 (B,H,W,F) must agree")
+    init = None
+    if idx_1_to_2_init is not None:
+        init = idx_1_to_2_init.to(torch.int64).reshape(b, h * w).contiguous()
+    dev = X11.device
+    idx = torch.empty((b, h * w), dtype=torch.int64, device=dev)
+    valid = torch.empty((b, h * w, 1), dtype=torch.bool, device=dev)
+    nbytes = lib.m3s_match_workspace_size(b, h, w, F)
+    ws = _lib.workspace("match", nbytes, dev)
+    _lib.check(lib.m3s_match(_lib.ptr(X11), _lib.ptr(X21), _lib.ptr(D11), _lib.ptr(D21), _lib.ptr(init),
+                             _lib.ptr(idx), _lib.ptr(valid), b, h, w, F, int(cfg["max_iter"]),
+                             float(cfg["lambda_init"]), float(cfg["convergence_thresh"]), float(cfg["dist_thresh"]),
+                             int(cfg["radius"]), int(cfg["dilation_max"]), _lib.ptr(ws), ws.numel(),
+                             _lib.stream_ptr(dev)))
+    return idx, valid

@@ -1,0 +1,217 @@
+"""``FrameTracker`` with the reference surface (``/root/reference/mast3r_slam/tracker.py:15-266``).
+
+``track(frame) -> (new_kf, match_info, try_reloc)`` keeps the reference's return triple and failure
+behaviour (low match fraction or Cholesky failure -> ``(False, [], True)``). The post-matching work
+— confidence / validity setup, the Sim(3) Gauss-Newton loop to convergence, the keyframe pointmap
+fusion and the keyframe-selection statistics — is ONE C-ABI call (``m3s_track``): 2 + 2*iters HIP
+kernels and a single host readback per frame, instead of ~30 torch launches and a ``.item()`` sync
+per GN iteration.
+
+``opt_pose_ray_dist_sim3`` / ``opt_pose_calib_sim3`` keep their reference signatures and run the
+same HIP GN kernels in "direct" mode; ``solve`` is the generic whitened normal-equation step of
+``tracker.py:156-171`` (torch ops on the device, not on the fused path).
+"""
+import ctypes
+
+import torch
+
+from m3s import _lib
+from m3s.config import config
+from m3s.matching import match
+from m3s.sim3 import Sim3
+
+
+def huber(r, k=1.345):
+    """nonlinear_optimizer.py:28-33."""
+    unit = torch.ones((1), dtype=r.dtype, device=r.device)
+    r_abs = torch.abs(r)
+    return torch.where(r_abs < k, unit, k / r_abs)
+
+
+def mast3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
+    """mast3r_utils.py:220-242 with the ViT call behind ``model.asymmetric_inference`` (stock
+    PyTorch-ROCm, out of scope); returns idx_i2j, valid_match_j, Xii, Cii, Qii, Xji, Cji, Qji."""
+    X, C, D, Q = model.asymmetric_inference(frame_i, frame_j)
+    b = X.shape[0] // 2
+    h, w = X.shape[1:3]
+    idx_i2j, valid_match_j = match(X[:b], X[b:], D[:b], D[b:], idx_1_to_2_init=idx_i2j_init)
+    Xr = X.reshape(2 * b, h * w, 3)
+    Cr = C.reshape(2 * b, h * w, 1)
+    Qr = Q.reshape(2 * b, h * w, 1)
+    return idx_i2j, valid_match_j, Xr[0], Cr[0], Qr[0], Xr[1], Cr[1], Qr[1]
+
+
+def _track_config(cfg, use_calib, img_size, K):
+    tc = _lib.TrackConfig()
+    tc.mode = 1 if use_calib else 0
+    tc.max_iters = int(cfg["max_iters"])
+    tc.C_conf, tc.Q_conf, tc.min_match_frac = float(cfg["C_conf"]), float(cfg["Q_conf"]), float(cfg["min_match_frac"])
+    if use_calib:
+        tc.sigma_a, tc.sigma_b = float(cfg["sigma_pixel"]), float(cfg["sigma_depth"])
+        Kh = K.detach().float().cpu().reshape(-1).tolist()
+        for i in range(9):
+            tc.K[i] = Kh[i]
+    else:
+        tc.sigma_a, tc.sigma_b = float(cfg["sigma_ray"]), float(cfg["sigma_dist"])
+    tc.huber_k, tc.rel_error, tc.delta_norm = float(cfg["huber"]), float(cfg["rel_error"]), float(cfg["delta_norm"])
+    tc.pixel_border, tc.depth_eps = float(cfg["pixel_border"]), float(cfg["depth_eps"])
+    tc.H, tc.W = int(img_size[0]), int(img_size[1])
+    return tc
+
+
+class FrameTracker:
+    def __init__(self, model, frames, device):
+        self.cfg = config["tracking"]
+        self.model = model
+        self.keyframes = frames
+        self.device = device
+        self.first_chunk = 8  # GN iterations enqueued before the first host readback
+        self.last_result = None
+        self.reset_idx_f2k()
+
+    def reset_idx_f2k(self):
+        self.idx_f2k = None
+
+    # ------------------------------------------------------------------ fused track
+    def track(self, frame):
+        """tracker.py:28-127."""
+        keyframe = self.keyframes.last_keyframe()
+        idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = mast3r_match_asymmetric(
+            self.model, frame, keyframe, idx_i2j_init=self.idx_f2k)
+        self.idx_f2k = idx_f2k.clone()
+        idx_f2k = idx_f2k[0]
+        valid_match_k = valid_match_k[0]
+        frame.update_pointmap(Xff, Cff)
+
+        use_calib = config["use_calib"]
+        img_size = frame.img_size
+        K = keyframe.K if use_calib else None
+        cfg = self.cfg
+        fuse_fused = cfg["filtering_mode"] == "weighted_pointmap"
+
+        res, T_out = self._run_track(
+            idx=idx_f2k, valid=valid_match_k, Xf=frame.X_canon, Cf=frame.C, Nf=frame.N, Qff=Qff,
+            Xk=keyframe.X_canon, Ck=keyframe.C, Nk=keyframe.N, Qkf=Qkf, T_WCf=frame.T_WC, T_WCk=keyframe.T_WC,
+            use_calib=use_calib, img_size=img_size, K=K,
+            fuse=(keyframe, Xkf, Ckf) if fuse_fused else None)
+
+        if res.status == _lib.TRACK_SKIPPED:
+            print(f"Skipped frame {frame.frame_id}")
+            return False, [], True
+        if res.status == _lib.TRACK_CHOLESKY_FAILED:
+            print(f"Cholesky failed {frame.frame_id}")
+            return False, [], True
+
+        frame.T_WC = Sim3(T_out[:8].view(1, 8).clone())
+        T_CkCf = Sim3(T_out[8:].view(1, 8).clone())
+        if fuse_fused:  # X/C fused in place on the device by m3s_track (frame.py:74-77)
+            keyframe.N += 1
+            keyframe.N_updates += 1
+        else:
+            keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf)
+        self.keyframes[len(self.keyframes) - 1] = keyframe
+
+        n = res.N
+        match_frac_k = res.n_valid_kf / n
+        unique_frac_f = res.n_unique / n
+        new_kf = min(match_frac_k, unique_frac_f) < cfg["match_frac_thresh"]
+        if new_kf:
+            self.reset_idx_f2k()
+        return (new_kf, [keyframe.X_canon, keyframe.get_average_conf(), frame.X_canon, frame.get_average_conf(),
+                         Qkf, Qff], False)
+
+    def _run_track(self, idx, valid, Xf, Cf, Nf, Qff, Xk, Ck, Nk, Qkf, T_WCf, T_WCk, use_calib, img_size, K,
+                   fuse=None, direct=False, meas_k=None, valid_meas_k=None, max_iters=None):
+        lib = _lib.load()
+        dev = Xf.device
+        _lib.require_cuda("track", Xf, Xk, Qff, valid)
+        cfg = dict(self.cfg)
+        if max_iters is not None:
+            cfg["max_iters"] = max_iters
+        tc = _track_config(cfg, use_calib, img_size, K)
+        N = tc.H * tc.W
+        c = lambda t, dt=torch.float32: None if t is None else t.to(dt).contiguous()
+        Xf, Xk, Qff, Qkf, Cf, Ck = c(Xf), c(Xk), c(Qff), c(Qkf), c(Cf), c(Ck)
+        idx = c(idx, torch.int64)
+        valid = valid.reshape(-1).to(torch.bool).contiguous()
+        meas_k = c(meas_k)
+        valid_meas_k = None if valid_meas_k is None else valid_meas_k.reshape(-1).to(torch.bool).contiguous()
+        TWf = T_WCf.data.reshape(8).float().contiguous()
+        TWk = T_WCk.data.reshape(8).float().contiguous()
+        for t in (Xf, Xk):
+            if t is not None and t.numel() != 3 * N:
+                raise RuntimeError("track: pointmaps must have H*W points")
+        ins = _lib.TrackInputs(
+            idx_f2k=_lib.ptr(idx).value, valid_match=_lib.ptr(valid).value, Xf=_lib.ptr(Xf).value,
+            Cf=_lib.ptr(Cf).value, Nf=float(Nf or 1), Qff=_lib.ptr(Qff).value, Xk=_lib.ptr(Xk).value,
+            Ck=_lib.ptr(Ck).value, Nk=float(Nk or 1), Qkf=_lib.ptr(Qkf).value, T_WCf=_lib.ptr(TWf).value,
+            T_WCk=_lib.ptr(TWk).value, direct=1 if direct else 0, meas_k=_lib.ptr(meas_k).value,
+            valid_meas_k=_lib.ptr(valid_meas_k).value)
+        fz = _lib.TrackFuse()
+        keep = []
+        if fuse is not None:
+            kf, Xkf, Ckf = fuse
+            if not (kf.X_canon.is_contiguous() and kf.C.is_contiguous() and kf.X_canon.dtype == torch.float32):
+                kf.X_canon = kf.X_canon.float().contiguous()
+                kf.C = kf.C.float().contiguous()
+            Xkf_c, Ckf_c = c(Xkf), c(Ckf)
+            keep += [Xkf_c, Ckf_c]
+            fz = _lib.TrackFuse(Xk_canon=_lib.ptr(kf.X_canon).value, Ck_sum=_lib.ptr(kf.C).value,
+                                Xkf=_lib.ptr(Xkf_c).value, Ckf=_lib.ptr(Ckf_c).value)
+        T_out = torch.empty(16, dtype=torch.float32, device=dev)
+        res = _lib.TrackResult()
+        ws = _lib.workspace("track", lib.m3s_track_workspace_size(N), dev)
+        _lib.check(lib.m3s_track(ctypes.byref(ins), ctypes.byref(tc), ctypes.byref(fz), int(self.first_chunk),
+                                 _lib.ptr(T_out), ctypes.byref(res), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)))
+        self.last_result = res
+        return res, T_out
+
+    # ------------------------------------------------------------------ reference method surface
+    def get_points_poses(self, frame, keyframe, idx_f2k, img_size, use_calib, K=None):
+        """tracker.py:129-154 (torch glue; the fused path does this inside track_setup)."""
+        from m3s.geometry import constrain_points_to_ray, get_pixel_coords
+
+        Xf, Xk = frame.X_canon, keyframe.X_canon
+        Cf, Ck = frame.get_average_conf(), keyframe.get_average_conf()
+        meas_k = valid_meas_k = None
+        if use_calib:
+            Xf = constrain_points_to_ray(img_size, Xf[None], K).squeeze(0)
+            Xk = constrain_points_to_ray(img_size, Xk[None], K).squeeze(0)
+            uv_k = get_pixel_coords(1, img_size, device=Xf.device, dtype=Xf.dtype).view(-1, 2)
+            meas_k = torch.cat((uv_k, torch.log(Xk[..., 2:3])), dim=-1)
+            valid_meas_k = Xk[..., 2:3] > self.cfg["depth_eps"]
+            meas_k[~valid_meas_k.repeat(1, 3)] = 0.0
+        return Xf[idx_f2k], Xk, frame.T_WC, keyframe.T_WC, Cf[idx_f2k], Ck, meas_k, valid_meas_k
+
+    def solve(self, sqrt_info, r, J):
+        """tracker.py:156-171 (generic step; raises on Cholesky failure like torch.linalg.cholesky)."""
+        whitened_r = sqrt_info * r
+        robust_sqrt_info = sqrt_info * torch.sqrt(huber(whitened_r, k=self.cfg["huber"]))
+        mdim = J.shape[-1]
+        A = (robust_sqrt_info[..., None] * J).view(-1, mdim)
+        b = (robust_sqrt_info * r).view(-1, 1)
+        H = A.T @ A
+        g = -A.T @ b
+        cost = 0.5 * (b.T @ b).item()
+        L = torch.linalg.cholesky(H, upper=False)
+        tau_j = torch.cholesky_solve(g, L, upper=False).view(1, -1)
+        return tau_j, cost
+
+    def _direct(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, use_calib, img_size, K, meas_k=None, valid_meas_k=None):
+        n = Xf.shape[0]
+        if img_size is None:
+            img_size = (1, n)
+        res, T_out = self._run_track(idx=None, valid=valid, Xf=Xf, Cf=None, Nf=1, Qff=Qk.reshape(-1), Xk=Xk, Ck=None,
+                                     Nk=1, Qkf=None, T_WCf=T_WCf, T_WCk=T_WCk, use_calib=use_calib,
+                                     img_size=img_size, K=K, direct=True, meas_k=meas_k, valid_meas_k=valid_meas_k)
+        if res.status == _lib.TRACK_CHOLESKY_FAILED:
+            raise RuntimeError("linalg.cholesky: The factorization could not be completed")
+        return Sim3(T_out[:8].view(1, 8).clone()), Sim3(T_out[8:].view(1, 8).clone())
+
+    def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
+        """tracker.py:173-214 -> (T_WCf, T_CkCf)."""
+        return self._direct(Xf, Xk, T_WCf, T_WCk, Qk, valid, False, None, None)
+
+    def opt_pose_calib_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, meas_k, valid_meas_k, K, img_size):
+        """tracker.py:216-266 -> (T_WCf, T_CkCf)."""
+        return self._direct(Xf, Xk, T_WCf, T_WCk, Qk, valid, True, img_size, K, meas_k, valid_meas_k)

@@ -1,0 +1,106 @@
+"""GPU parity: tracking GN (FrameTracker.track, opt_pose_*) vs the reference glue's golden vectors.
+
+Contract (BASELINE.json north_star): pose/points to 1e-5 for identical inputs. The golden vectors
+come from the reference's own tracker.py run on the same synthetic inputs (make_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(g, use_calib, N, H, W):
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+
+    config["use_calib"] = use_calib
+    dev = "cuda"
+    kf = Frame(0, (H, W), T_WC=Sim3(torch.from_numpy(g["T_WCk"]).view(1, 8).to(dev)))
+    kf.K = torch.from_numpy(g["K"]).to(dev)
+    kf.update_pointmap(torch.from_numpy(g["Xk"]).to(dev), torch.from_numpy(g["Ck"]).to(dev))
+    frame = Frame(1, (H, W), T_WC=Sim3(kf.T_WC.data.clone()))
+    kfs = Keyframes()
+    kfs.append(kf)
+
+    class Model:
+        def asymmetric_inference(self, fi, fj):
+            return (torch.from_numpy(g["X"]).to(dev), torch.from_numpy(g["C"]).to(dev),
+                    torch.from_numpy(g["D"]).to(dev), torch.from_numpy(g["Q"]).to(dev))
+
+    return kf, frame, kfs, Model()
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_track_matches_reference(golden, mode):
+    from m3s.tracker import FrameTracker
+
+    g = golden("tracking_48x64.npz")
+    H, W = 48, 64
+    kf, frame, kfs, model = _setup(g, mode == "calib", H * W, H, W)
+    tr = FrameTracker(model, kfs, "cuda")
+    new_kf, info, reloc = tr.track(frame)
+    assert bool(new_kf) == bool(g[f"{mode}_new_kf"]) and bool(reloc) == bool(g[f"{mode}_reloc"])
+    assert tr.last_result.iters == int(g[f"{mode}_iters"])
+    np.testing.assert_allclose(frame.T_WC.data.cpu().numpy(), g[f"{mode}_T_WCf"], atol=1e-5)
+    np.testing.assert_allclose(kf.X_canon.cpu().numpy(), g[f"{mode}_kf_X"], atol=1e-5)
+    np.testing.assert_allclose(kf.C.cpu().numpy(), g[f"{mode}_kf_C"], atol=1e-5)
+    assert kf.N == 2
+    assert len(info) == 6
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_opt_pose_matches_reference(golden, mode):
+    from m3s.sim3 import Sim3
+    from m3s.tracker import FrameTracker
+
+    g = golden("optpose_32x48.npz")
+    d = lambda k: torch.from_numpy(g[k]).cuda()
+    tr = FrameTracker(None, None, "cuda")
+    if mode == "rays":
+        Tf, Tr = tr.opt_pose_ray_dist_sim3(d("Xf"), d("Xk"), Sim3(d("T_WCf")), Sim3(d("T_WCk")), d("Qk"), d("valid"))
+    else:
+        Tf, Tr = tr.opt_pose_calib_sim3(d("Xf_c"), d("Xk"), Sim3(d("T_WCf")), Sim3(d("T_WCk")), d("Qk"), d("valid"),
+                                        d("meas"), d("vmeas"), d("K"), (32, 48))
+    np.testing.assert_allclose(Tf.data.cpu().numpy(), g[f"{mode}_T_WCf"], atol=1e-5)
+    np.testing.assert_allclose(Tr.data.cpu().numpy(), g[f"{mode}_T_CkCf"], atol=1e-5)
+
+
+def test_track_skips_low_match_fraction(golden):
+    """tracker.py:67-70: match_frac < min_match_frac -> (False, [], True), keyframe untouched."""
+    from m3s.config import config
+    from m3s.tracker import FrameTracker
+
+    g = golden("tracking_48x64.npz")
+    kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+    config["tracking"]["Q_conf"] = 1e9  # nothing passes the Q test
+    X0 = kf.X_canon.clone()
+    tr = FrameTracker(model, kfs, "cuda")
+    assert tr.track(frame) == (False, [], True)
+    assert torch.equal(kf.X_canon, X0) and kf.N == 1
+
+
+def test_track_full_size_converges_to_ground_truth():
+    """512x512 synthetic pair: the tracked relative pose recovers the generating T_CkCf."""
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    P = make_pair(512, 512, seed=2)
+    model = SyntheticModel([P], "cuda")
+    kf = Frame(0, (512, 512))
+    kf.T_WC = Sim3.Identity(1, device="cuda")
+    kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
+    kfs = Keyframes()
+    kfs.append(kf)
+    tr = FrameTracker(model, kfs, "cuda")
+    frame = Frame(1, (512, 512), T_WC=Sim3.Identity(1, device="cuda"))
+    new_kf, info, reloc = tr.track(frame)
+    assert not reloc
+    T = frame.T_WC.data.cpu().numpy()[0]
+    T_gt = P["T_gt"].numpy()
+    assert np.abs(T[:3] - T_gt[:3]).max() < 2e-3
+    assert abs(T[7] - T_gt[7]) < 2e-3
+    assert abs(abs(float(np.dot(T[3:7], T_gt[3:7]))) - 1.0) < 1e-5

@@ -1,0 +1,138 @@
+"""CPU: host logic, the C-ABI library surface, the Sim3 stand-in and config handling."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import oracle.oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_abi_library_exports_every_declared_symbol():
+    from m3s import _lib
+
+    header = open(os.path.join(REPO, "include", "m3s.h")).read()
+    declared = set(re.findall(r"\b(m3s_[a-z0-9_]+)\s*\(", header))
+    assert declared, "no declarations parsed"
+    lib = ctypes.CDLL(_lib.LIB_PATH)  # loads without a GPU
+    missing = [s for s in sorted(declared) if not hasattr(lib, s)]
+    assert not missing, missing
+    assert declared == set(_lib.EXPORTED)  # the ctypes table binds exactly the header
+    lib.m3s_abi_version.restype = ctypes.c_int
+    assert lib.m3s_abi_version() == 1
+
+
+def test_workspace_sizes_are_monotone():
+    from m3s import _lib
+
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name, args in (("m3s_match_workspace_size", [(1, 64, 64, 24), (2, 64, 64, 24), (1, 512, 512, 24)]),
+                       ("m3s_track_workspace_size", [(1024,), (4096,), (262144,)]),
+                       ("m3s_ba_workspace_size", [(4, 1024, 6), (8, 1024, 20), (256, 196608, 2000)])):
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_size_t
+        sizes = [fn(*a) for a in args]
+        assert sizes == sorted(sizes) and sizes[0] > 0
+
+
+def test_backends_reject_like_reference_and_never_fall_back():
+    import mast3r_slam_backends as B
+
+    rays = torch.zeros(1, 8, 8, 9).transpose(1, 2)
+    with pytest.raises(RuntimeError, match="must be contiguous"):
+        B.iter_proj(rays, torch.zeros(1, 64, 3), torch.zeros(1, 64, 2), 10, 1e-8, 1e-6)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="no HIP device"):
+            B.iter_proj(torch.zeros(1, 8, 8, 9), torch.zeros(1, 64, 3), torch.zeros(1, 64, 2), 10, 1e-8, 1e-6)
+        with pytest.raises(RuntimeError, match="no HIP device"):
+            B.refine_matches(torch.zeros(1, 8, 8, 24, dtype=torch.float16), torch.zeros(1, 64, 24, dtype=torch.float16),
+                             torch.zeros(1, 64, 2, dtype=torch.int64), 3, 5)
+
+
+def _shim():
+    import oracle.lietorch_shim as shim
+
+    return shim
+
+
+def test_sim3_matches_oracle_shim_and_fp64():
+    from m3s.sim3 import Sim3
+
+    shim = _shim()
+    g = torch.Generator().manual_seed(0)
+    xi = torch.randn(16, 7, generator=g) * torch.tensor([0.3, 0.3, 0.3, 0.5, 0.5, 0.5, 0.2])
+    xi[0] = 0
+    xi[1, 3:6] = 1e-5  # small-angle branch
+    xi[2, 6] = 1e-8  # |sigma| < EPS branch
+    a = Sim3.exp(xi)
+    b = shim.Sim3.exp(xi)
+    np.testing.assert_allclose(a.data.numpy(), b.data.numpy(), atol=2e-6)
+    for k in range(16):
+        # the float closed form (lietorch / gn_kernels.cu:360-372) cancels for small theta & sigma:
+        # vs the fp64 truth only ~1e-4; vs the float restatement tightly
+        np.testing.assert_allclose(a.data[k].numpy(), O.sim3_exp(xi[k].double().numpy()), atol=1e-4)
+        np.testing.assert_allclose(a.data[k].numpy(), O.exp_sim3_f32(xi[k].numpy()), atol=2e-6)
+    p = torch.randn(16, 5, 3, generator=g)
+    T1, T2 = Sim3.exp(xi), Sim3.exp(xi.flip(0))
+    np.testing.assert_allclose((T1 * T2).act(p).numpy(), T1.act(T2.act(p)).numpy(), atol=2e-5)
+    np.testing.assert_allclose((T1.inv() * T1).data.numpy(), Sim3.Identity(16).data.numpy(), atol=2e-6)
+    np.testing.assert_allclose(T1.retr(xi.flip(0)).data.numpy(), (Sim3.exp(xi.flip(0)) * T1).data.numpy(), atol=1e-6)
+    M = T1.matrix()
+    ph = torch.cat((p, torch.ones(16, 5, 1)), -1)
+    np.testing.assert_allclose((M[:, None] @ ph[..., None])[..., :3, 0].numpy(), T1.act(p).numpy(), atol=2e-5)
+
+
+def test_config_loads_reference_style_yaml(tmp_path):
+    from m3s.config import config, load_config
+
+    base = tmp_path / "base.yaml"
+    base.write_text("matching:\n  radius: 2\n  lambda_init: 1e-7\ntracking:\n  sigma_ray: 5e-3\n")
+    child = tmp_path / "child.yaml"
+    child.write_text(f'inherit: "{base}"\nuse_calib: True\ndataset:\n  subsample: 2\n')
+    load_config(str(child))
+    assert config["use_calib"] is True and config["matching"]["radius"] == 2
+    assert isinstance(config["matching"]["lambda_init"], float) and config["matching"]["lambda_init"] == 1e-7
+    assert config["tracking"]["sigma_ray"] == 5e-3 and config["tracking"]["max_iters"] == 50  # defaults kept
+    assert config["dataset"]["subsample"] == 2
+
+
+def test_shard_range_partitions_edges():
+    from m3s.dist_ba import shard_range
+
+    for E in (0, 1, 7, 2000, 2001):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(E, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == E
+            assert all(rs[r][1] == rs[r + 1][0] for r in range(world - 1))
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_frame_weighted_fusion_matches_reference_formula():
+    from m3s.frame import Frame
+
+    g = torch.Generator().manual_seed(0)
+    f = Frame(0, (4, 4))
+    X1, C1 = torch.randn(16, 3, generator=g), torch.rand(16, 1, generator=g) + 1
+    X2, C2 = torch.randn(16, 3, generator=g), torch.rand(16, 1, generator=g) + 1
+    f.update_pointmap(X1, C1)
+    f.update_pointmap(X2, C2)
+    assert f.N == 2 and f.N_updates == 2
+    torch.testing.assert_close(f.X_canon, (C1 * X1 + C2 * X2) / (C1 + C2))
+    torch.testing.assert_close(f.get_average_conf(), (C1 + C2) / 2)
+
+
+def test_synthetic_pair_is_consistent():
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import make_pair
+
+    P = make_pair(32, 48, seed=0, noise=0.0)
+    X21 = P["X"][1].reshape(-1, 3)
+    np.testing.assert_allclose(Sim3(P["T_gt"].view(1, 8)).act(X21).numpy(), P["Xk"].numpy(), atol=1e-5)
+    D = P["D"]
+    np.testing.assert_allclose(D.norm(dim=-1).numpy(), 1.0, atol=1e-5)
+    assert (P["Q"] > 1.0).all() and (P["C"] > 1.0).all()
