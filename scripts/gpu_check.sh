@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU-box check used during development: smoke, GPU parity tests. Each step time-limited.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "SMOKE_RC=$rc"; tail -5 gpurun_out/smoke.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "PYTEST_RC=$rc"; tail -40 gpurun_out/pytest_gpu.log
+exit $rc
