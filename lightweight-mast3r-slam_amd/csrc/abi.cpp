@@ -224,11 +224,12 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
 // ------------------------------------------------------------------------------------------
 // tracking
 // ------------------------------------------------------------------------------------------
-static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }
+// GN blocks: 2 points per lane at 512x512 (512 blocks = 2 per CU), at most 512 partials to reduce
+static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
 
-static size_t track_carve(Carver& c, int N, TrackState** st, uint32_t** bitmap, double** partials, float** rec) {
+static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, double** partials, float** rec) {
   *st = c.take<TrackState>(1);
-  *bitmap = c.take<uint32_t>((size_t)(N + 31) / 32);
+  *flags = c.take<uint8_t>(((size_t)N + 15) / 16 * 16);
   *partials = c.take<double>((size_t)track_nparts(N) * 40);
   *rec = c.take<float>((size_t)N * 8);
   return c.off;
@@ -237,7 +238,7 @@ static size_t track_carve(Carver& c, int N, TrackState** st, uint32_t** bitmap, 
 extern "C" size_t m3s_track_workspace_size(int N) {
   Carver c(nullptr);
   TrackState* st;
-  uint32_t* bm;
+  uint8_t* bm;
   double* pa;
   float* rec;
   return track_carve(c, N, &st, &bm, &pa, &rec);
@@ -265,7 +266,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   Carver c(workspace);
   TrackArgs a;
   TrackState* st;
-  track_carve(c, N, &st, &a.bitmap, &a.partials, &a.rec);
+  track_carve(c, N, &st, &a.flags, &a.partials, &a.rec);
   a.state = st;
   a.idx = in->idx_f2k;
   a.valid_match = in->valid_match;
@@ -304,9 +305,9 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   p.cy = cfg->K[5];
   if (p.mode == 1) M3S_CHECK(p.fx != 0.0f && p.fy != 0.0f, "track: calib mode needs K");
   hipStream_t s = (hipStream_t)stream;
-  const size_t bitmap_bytes = ((size_t)(N + 31) / 32) * 4;
+  const size_t flag_bytes = ((size_t)N + 15) / 16 * 16;
   HIP_TRY(hipMemsetAsync(st, 0, sizeof(TrackState), s), "track memset");
-  HIP_TRY(hipMemsetAsync(a.bitmap, 0, bitmap_bytes, s), "track memset");
+  HIP_TRY(hipMemsetAsync(a.flags, 0, flag_bytes, s), "track memset");
   HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, s), "track init launch");
   {
     Span sp("track_setup", s);

@@ -21,7 +21,8 @@ struct TrackState {
   int n_valid_opt;
   int n_valid_kf;
   int n_unique;
-  int pad[2];
+  int arrive;  // per-iteration block-arrival ticket of the fused GN kernel (last arriver solves)
+  int pad;
 };
 
 struct TrackParams {
@@ -49,7 +50,7 @@ struct TrackArgs {
   const float* meas_k;         // (N,3) direct calib only
   const uint8_t* valid_meas;   // (N)   direct calib only
   float* rec;                 // (N,8) per-point GN record (workspace)
-  uint32_t* bitmap;            // (ceil(N/32)) unique(idx) bitmap (workspace, zeroed per frame)
+  uint8_t* flags;              // (N, padded to 16) unique(idx[valid]) byte map (workspace, zeroed per frame)
   double* partials;            // (nparts, 40) block partial sums (workspace)
   TrackState* state;
 };

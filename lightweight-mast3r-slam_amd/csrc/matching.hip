@@ -10,12 +10,12 @@
 //
 // This file is compiled with -ffp-contract=off: the refine score must round every half product and
 // every half add separately (c10::Half operator* / operator+), which a contracted v_fma_f16 breaks.
-#include "m3s_common.hpp"
+#include "m3s_half.hpp"
+
+extern "C" hipError_t m3s_launch_refine_tile(const void*, const void*, const void*, void*, int, int, int, int, int,
+                                             int, int, hipStream_t);
 
 namespace m3s {
-
-typedef _Float16 h1;
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------
 // prep: rays = X/max(|X|,1e-12); gx, gy = Scharr/32 with reflect padding; out (B,H,W,9).
@@ -231,30 +231,6 @@ __device__ __forceinline__ h1 score_f16(const h2* q, const h1* __restrict__ c) {
   return s;
 }
 
-// D21 row source: f16 (reference signature, caller did .half()) or f32 (fused path: convert here).
-template <int F, bool D21_F32>
-__device__ __forceinline__ void load_query(const void* D21, size_t row, h2* q) {
-  if constexpr (D21_F32) {
-    const float4* s = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(D21) + row * F);
-#pragma unroll
-    for (int k = 0; k < F / 4; k++) {
-      const float4 v = s[k];
-      q[2 * k + 0] = h2{(h1)v.x, (h1)v.y};
-      q[2 * k + 1] = h2{(h1)v.z, (h1)v.w};
-    }
-  } else {
-    const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const h1*>(D21) + row * F);
-#pragma unroll
-    for (int k = 0; k < F / 8; k++) {
-      const uint4 t = s[k];
-      q[4 * k + 0] = *reinterpret_cast<const h2*>(&t.x);
-      q[4 * k + 1] = *reinterpret_cast<const h2*>(&t.y);
-      q[4 * k + 2] = *reinterpret_cast<const h2*>(&t.z);
-      q[4 * k + 3] = *reinterpret_cast<const h2*>(&t.w);
-    }
-  }
-}
-
 template <int F>
 __device__ __forceinline__ void refine_point(const h1* __restrict__ img, int H, int W, const h2* q, int radius,
                                              int dilation_max, int& u0, int& v0) {
@@ -390,6 +366,9 @@ extern "C" hipError_t m3s_launch_refine_f16(const void* D11, const void* D21, co
   dim3 grid((N + 255) / 256, B);
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11);
   const m3s::h1* q = reinterpret_cast<const m3s::h1*>(D21);
+  if (N == H * W && m3s_launch_refine_tile(D11, D21, p1, p1_new, B, H, W, F, radius, dilation_max, 0, s) ==
+                        hipSuccess)
+    return hipSuccess;  // tiled LDS path (query n is pixel n of the grid)
   switch (F) {
     case 24:
       hipLaunchKernelGGL(m3s::refine_f16_kernel<24>, grid, dim3(256), 0, s, a, q, p1, p1_new, H, W, N, radius,
@@ -422,6 +401,8 @@ extern "C" hipError_t m3s_launch_refine_lin(const void* D11h, const float* D21, 
                                             int H, int W, int F, int radius, int dilation_max, hipStream_t s) {
   dim3 grid((H * W + 255) / 256, B);
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
+  if (radius > 0 && m3s_launch_refine_tile(D11h, D21, p1, idx_out, B, H, W, F, radius, dilation_max, 1, s) == hipSuccess)
+    return hipSuccess;  // tiled LDS path
   switch (F) {
     case 24:
       hipLaunchKernelGGL(m3s::refine_lin_kernel<24>, grid, dim3(256), 0, s, a, D21, p1, idx_out, H, W, radius,

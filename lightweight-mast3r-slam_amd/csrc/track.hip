@@ -10,12 +10,16 @@
 //   keyframe fusion + selection stats  tracker.py:95-114, frame.py:41-77 (weighted_pointmap)
 //
 // Device pipeline per frame, no host synchronisation inside:
-//   track_setup  : gather Xf[idx], Qk = sqrt(Qff[idx] Qkf), validity masks, per-point GN record,
-//                  counts (valid_opt, valid_kf) and the unique(idx[valid]) bitmap
-//   gn_lin (xI)  : 256-thread blocks, fp64 accumulation of the 28 (H upper) + 7 (g) + 1 (cost) sums
-//   gn_solve (xI): one block: fp64 partial reduction, 7x7 Cholesky, tau, T <- Exp(tau) T,
-//                  convergence test, T_WCf = T_WCk T_CkCf; later launches exit immediately
-//   fuse         : keyframe X <- (C X + C' T_CkCf Xkf) / (C + C'), C += C' when tracking succeeded
+//   track_init   : T_CkCf = T_WCk^-1 T_WCf into the device state
+//   track_setup  : gather Xf[idx], Qk = sqrt(Qff[idx] Qkf), validity masks, a 32-byte per-point GN
+//                  record, counts (valid_opt, valid_kf) and the unique(idx[valid]) byte map
+//   track_count  : popcount of the byte map (torch.unique(...).shape[0], tracker.py:106-108)
+//   gn_iter (xI) : ONE launch per GN iteration: every block accumulates the 28 (H upper) + 7 (g)
+//                  + 1 (cost) sums in fp64, publishes them write-through (sc1) and takes an arrival
+//                  ticket; the last-arriving block reduces all partials, solves the 7x7 system in
+//                  fp64, retracts T <- Exp(tau) T, applies the convergence test and, once done,
+//                  writes T_WCf = T_WCk T_CkCf. Later launches exit at their first load.
+//   fuse         : keyframe X <- (C X + C' T_CkCf Xkf) / (C + C'), C += C'
 #include "m3s_common.hpp"
 #include "m3s_track.h"
 
@@ -56,6 +60,20 @@ __device__ __forceinline__ void sim3_inv(const float* A, float* C) {
   C[7] = si;
 }
 
+// state <- {T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}
+__global__ void track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk) {
+  if (threadIdx.x != 0) return;
+  float Ti[8], Tf[8], Tk[8];
+  for (int c = 0; c < 8; c++) {
+    Tf[c] = T_WCf[c];
+    Tk[c] = T_WCk[c];
+    st->T_WCk[c] = Tk[c];
+  }
+  sim3_inv(Tk, Ti);
+  sim3_mul_norm(Ti, Tf, st->T);
+  st->old_cost = __builtin_inf();
+}
+
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -88,7 +106,7 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
     const bool valid_opt = vm && (cf > p.C_conf) && (ck > p.C_conf) && (qk > p.Q_conf);
     v_opt = valid_opt;
     v_kf = vm && (qk > p.Q_conf);
-    if (vm) atomicOr(&a.bitmap[i >> 5], 1u << (i & 31));
+    if (vm) a.flags[i] = 1;  // benign same-value races; counted by track_count_kernel
     const float sq = valid_opt ? sqrtf(qk) : 0.0f;
     float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
     const float* Xf = a.Xf + i * 3;
@@ -123,6 +141,21 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
     atomicAdd(&a.state->n_valid_opt, s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3]);
     atomicAdd(&a.state->n_valid_kf, s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3]);
   }
+}
+
+// number of distinct idx among valid matches = nonzero bytes of the flag map (16 bytes per lane-load)
+__global__ void __launch_bounds__(256) track_count_kernel(const uint4* __restrict__ flags, int n16,
+                                                          TrackState* __restrict__ st) {
+  int cnt = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
+    const uint4 v = flags[i];
+    cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // flags are 0/1 bytes
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  __shared__ int s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&st->n_unique, s[0] + s[1] + s[2] + s[3]);
 }
 
 __device__ __forceinline__ bool track_skipped(const TrackState* st, const TrackParams& p) {
@@ -162,159 +195,54 @@ __device__ __forceinline__ void chain_row(const float dh[3], const float Y[3], f
   J[6] = -(dh[0] * Y[0] + dh[1] * Y[1] + dh[2] * Y[2]);
 }
 
-__global__ void __launch_bounds__(256) gn_lin_kernel(TrackArgs a, TrackParams p) {
-  const TrackState* st = a.state;
-  if (st->done || track_skipped(st, p)) return;
-  float T[8];
-#pragma unroll
-  for (int c = 0; c < 8; c++) T[c] = st->T[c];
-  double acc[GN_NSUM];
-#pragma unroll
-  for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
-  const float4* rec = reinterpret_cast<const float4*>(a.rec);
-  const int stride = gridDim.x * blockDim.x;
-  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < p.N; n += stride) {
-    const float4 r0 = rec[2 * (size_t)n], r1 = rec[2 * (size_t)n + 1];
-    const float X[3] = {r0.x, r0.y, r0.z};
-    float Y[3];
-    actSim3(T, X, Y);
-    const float sq = r1.w;
-    if (p.mode == 0) {
-      const float d = sqrtf(Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2]);
-      const float di = 1.0f / d;
-      const float di2 = di * di;
-      const float rr[3] = {di * Y[0], di * Y[1], di * Y[2]};
-      const float res[4] = {r0.w - rr[0], r1.x - rr[1], r1.y - rr[2], r1.z - d};
-      const float si_r = p.c_a * sq, si_d = p.c_b * sq;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        float dh[3];
-#pragma unroll
-        for (int m = 0; m < 3; m++) dh[m] = di * ((k == m ? 1.0f : 0.0f) - di2 * (Y[k] * Y[m]));
-        float J[7];
-        chain_row(dh, Y, J);
-        acc_row(acc, J, res[k], si_r, p.huber_k);
-      }
-      float J[7];
-      chain_row(rr, Y, J);
-      acc_row(acc, J, res[3], si_d, p.huber_k);
-    } else {
-      const float x = Y[0], y = Y[1], z = Y[2];
-      const float pu = p.K[0] * x + p.K[1] * y + p.K[2] * z;
-      const float pv = p.K[3] * x + p.K[4] * y + p.K[5] * z;
-      const float pw = p.K[6] * x + p.K[7] * y + p.K[8] * z;
-      const float u = pu / pw, v = pv / pw;
-      const bool valid_z = z > p.depth_eps;
-      const float logz = valid_z ? logf(z) : 0.0f;
-      const bool valid = (u > p.pixel_border) && (u < (float)(p.W - 1) - p.pixel_border) &&
-                         (v > p.pixel_border) && (v < (float)(p.H - 1) - p.pixel_border) && valid_z &&
-                         (r1.z != 0.0f);
-      const float vf = valid ? 1.0f : 0.0f;
-      const float si_p = vf * (p.c_a * sq), si_z = vf * (p.c_b * sq);
-      const float zi = 1.0f / z;
-      const float res[3] = {r0.w - u, r1.x - v, r1.y - logz};
-      float dh[3], J[7];
-      dh[0] = p.K[0] * zi;
-      dh[1] = 0.0f;
-      dh[2] = (-p.K[0] * x * zi) * zi;
-      chain_row(dh, Y, J);
-      acc_row(acc, J, res[0], si_p, p.huber_k);
-      dh[0] = 0.0f;
-      dh[1] = p.K[4] * zi;
-      dh[2] = (-p.K[4] * y * zi) * zi;
-      chain_row(dh, Y, J);
-      acc_row(acc, J, res[1], si_p, p.huber_k);
-      dh[0] = 0.0f;
-      dh[1] = 0.0f;
-      dh[2] = zi;
-      chain_row(dh, Y, J);
-      acc_row(acc, J, res[2], si_z, p.huber_k);
-    }
-  }
-  // wave64 butterfly, then the 4 waves through LDS; fp64 throughout
-  __shared__ double s_part[4][GN_NSUM];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < GN_NSUM; c++) {
-    const double v = wave_sum(acc[c]);
-    if (lane == 0) s_part[wid][c] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < GN_NSUM) {
-    const int c = threadIdx.x;
-    a.partials[(size_t)blockIdx.x * GN_PSTRIDE + c] = s_part[0][c] + s_part[1][c] + s_part[2][c] + s_part[3][c];
-  }
-}
-
-// 7x7 fp64 Cholesky solve H tau = g; false when H is not positive definite (torch.linalg.cholesky raises)
-__device__ bool chol7(double H[7][7], double g[7], double tau[7]) {
-  double L[7][7];
+// 7x7 Cholesky solve H tau = g in fp32 (torch.linalg.cholesky / cholesky_solve on the float32 H of
+// tracker.py:168-169); false when H is not positive definite (torch raises). The normal equations
+// themselves are accumulated in fp64; only this tiny serial tail runs in fp32, where div/sqrt are
+// short instruction sequences (the fp64 ones dominated the single-lane tail).
+__device__ bool chol7(const double Hd[7][7], const double gd[7], double tau[7]) {
+  float L[7][7];
   for (int j = 0; j < 7; j++) {
-    double d = H[j][j];
+    float d = (float)Hd[j][j];
     for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
-    if (!(d > 0.0)) return false;
-    d = sqrt(d);
+    if (!(d > 0.0f)) return false;
+    d = sqrtf(d);
     L[j][j] = d;
+    const float dinv = 1.0f / d;
     for (int i = j + 1; i < 7; i++) {
-      double s = H[i][j];
+      float s = (float)Hd[i][j];
       for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
-      L[i][j] = s / d;
+      L[i][j] = s * dinv;
     }
   }
-  double y[7];
+  float y[7], t[7];
   for (int i = 0; i < 7; i++) {
-    double s = g[i];
+    float s = (float)gd[i];
     for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
     y[i] = s / L[i][i];
   }
   for (int i = 6; i >= 0; i--) {
-    double s = y[i];
-    for (int k = i + 1; k < 7; k++) s -= L[k][i] * tau[k];
-    tau[i] = s / L[i][i];
+    float s = y[i];
+    for (int k = i + 1; k < 7; k++) s -= L[k][i] * t[k];
+    t[i] = s / L[i][i];
   }
+  for (int i = 0; i < 7; i++) tau[i] = t[i];
   return true;
 }
 
-__global__ void __launch_bounds__(256) gn_solve_kernel(TrackArgs a, TrackParams p, int nparts) {
-  TrackState* st = a.state;
-  __shared__ double s_sum[GN_NSUM];
-  __shared__ int s_bits[4];
-  if (st->iter == 0 && st->n_unique < 0) {  // unique(idx[valid_match]) count, once per frame
-    int cnt = 0;
-    for (int w = threadIdx.x; w < (p.N + 31) / 32; w += blockDim.x) cnt += __popc(a.bitmap[w]);
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-    if ((threadIdx.x & 63) == 0) s_bits[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) st->n_unique = s_bits[0] + s_bits[1] + s_bits[2] + s_bits[3];
-  }
-  if (st->done) return;
-  if (track_skipped(st, p)) {
-    if (threadIdx.x == 0) {
-      st->status = M3S_TRACK_SKIPPED;
-      st->done = 1;
-    }
-    return;
-  }
-  // column-parallel fp64 reduction of the block partials: wave w owns columns w, w+4, ...
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int c = wid; c < GN_NSUM; c += 4) {
-    double v = 0.0;
-    for (int r = lane; r < nparts; r += 64) v += a.partials[(size_t)r * GN_PSTRIDE + c];
-    v = wave_sum(v);
-    if (lane == 0) s_sum[c] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+// one thread: H, g, cost -> tau -> T update + convergence (tracker.py:156-171, 186-209).
+// T, iter and old_cost come in registers (loaded at kernel start, not re-read on the serial tail).
+__device__ void gn_finish(TrackState* st, const TrackParams& p, const double* sum, const float* T, int iter,
+                          double old) {
   double H[7][7], g[7], tau[7];
   int l = 0;
   for (int c = 0; c < 7; c++)
     for (int d = c; d < 7; d++) {
-      H[c][d] = s_sum[l];
-      H[d][c] = s_sum[l];
+      H[c][d] = sum[l];
+      H[d][c] = sum[l];
       l++;
     }
-  for (int c = 0; c < 7; c++) g[c] = s_sum[28 + c];
-  const double cost = s_sum[35];
+  for (int c = 0; c < 7; c++) g[c] = sum[28 + c];
+  const double cost = sum[35];
   st->last_cost = cost;
   if (!chol7(H, g, tau)) {
     st->status = M3S_TRACK_CHOLESKY_FAILED;
@@ -329,23 +257,210 @@ __global__ void __launch_bounds__(256) gn_solve_kernel(TrackArgs a, TrackParams 
   }
   float E[8], Tn[8];
   expSim3(tf, E);
-  sim3_mul_norm(E, st->T, Tn);  // T_CkCf.retr(tau) = Exp(tau) * T_CkCf
+  sim3_mul_norm(E, T, Tn);  // T_CkCf.retr(tau) = Exp(tau) * T_CkCf
   for (int c = 0; c < 8; c++) st->T[c] = Tn[c];
-  const int it = st->iter + 1;
+  const int it = iter + 1;
   st->iter = it;
-  const double old = st->old_cost;
   const double rel = fabs((old - cost) / old);  // inf/inf = nan on the first step -> false
   const bool conv = (rel < (double)p.rel_error) || (sqrtf(tn2) < p.delta_norm);
   st->old_cost = cost;
   if (conv || it >= p.max_iters) {
     st->status = conv ? M3S_TRACK_OK : M3S_TRACK_MAX_ITERS;
     st->done = 1;
+    float Tk[8];
+    for (int c = 0; c < 8; c++) Tk[c] = st->T_WCk[c];
+    sim3_mul_norm(Tk, Tn, st->T_WCf);  // T_WCf = T_WCk * T_CkCf
   }
-  if (st->done) sim3_mul_norm(st->T_WCk, st->T, st->T_WCf);  // T_WCf = T_WCk * T_CkCf
 }
 
-// keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77), only when
-// tracking succeeded; X_kf, C_kf updated in place.
+#ifdef M3S_GN_STAMPS  // (experiment builds only) s_memrealtime stamps of block 0 / the last block
+__device__ unsigned long long g_gn_stamps[8 * 16];
+#define GN_STAMP(k)                                                                                \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && iter0 < 8) g_gn_stamps[iter0 * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define GN_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) int gint;
+
+#define GN_THREADS 256
+#define GN_PPT 4     // points per thread per round: all their record loads issued before any math
+#define GN_LDS_LD 37  // row pitch (doubles) of the transpose buffer: 36 sums + 1 pad
+
+// Deterministic block sum of 36 fp64 values per thread through an LDS transpose: thread t writes
+// its row, then 7 groups x 36 columns of threads sum fixed row subsets, then 36 threads add the 7
+// group sums in order. Replaces 36 six-step shuffle butterflies (measured ~8 us per launch).
+__device__ __forceinline__ void block_sum36(const double* v, double (*s_all)[GN_LDS_LD], double (*s_grp)[GN_NSUM],
+                                            double* out) {
+#pragma unroll
+  for (int c = 0; c < GN_NSUM; c++) s_all[threadIdx.x][c] = v[c];
+  __syncthreads();
+  if (threadIdx.x < 7 * GN_NSUM) {
+    const int c = threadIdx.x % GN_NSUM, g = threadIdx.x / GN_NSUM;
+    double a0 = 0.0, a1 = 0.0;
+    int r = g;
+    for (; r + 7 < GN_THREADS; r += 14) {
+      a0 += s_all[r][c];
+      a1 += s_all[r + 7][c];
+    }
+    if (r < GN_THREADS) a0 += s_all[r][c];
+    s_grp[g][c] = a0 + a1;
+  }
+  __syncthreads();
+  if (threadIdx.x < GN_NSUM) {
+    const int c = threadIdx.x;
+    out[c] = (((((s_grp[0][c] + s_grp[1][c]) + s_grp[2][c]) + s_grp[3][c]) + s_grp[4][c]) + s_grp[5][c]) + s_grp[6][c];
+  }
+}
+
+__device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, float4 r0, float4 r1, double* acc) {
+  const float X[3] = {r0.x, r0.y, r0.z};
+  float Y[3];
+  actSim3(T, X, Y);
+  const float sq = r1.w;
+  if (p.mode == 0) {
+    const float d = sqrtf(Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2]);
+    const float di = 1.0f / d;
+    const float di2 = di * di;
+    const float rr[3] = {di * Y[0], di * Y[1], di * Y[2]};
+    const float res[4] = {r0.w - rr[0], r1.x - rr[1], r1.y - rr[2], r1.z - d};
+    const float si_r = p.c_a * sq, si_d = p.c_b * sq;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float dh[3];
+#pragma unroll
+      for (int m = 0; m < 3; m++) dh[m] = di * ((k == m ? 1.0f : 0.0f) - di2 * (Y[k] * Y[m]));
+      float J[7];
+      chain_row(dh, Y, J);
+      acc_row(acc, J, res[k], si_r, p.huber_k);
+    }
+    float J[7];
+    chain_row(rr, Y, J);
+    acc_row(acc, J, res[3], si_d, p.huber_k);
+  } else {
+    const float x = Y[0], y = Y[1], z = Y[2];
+    const float pu = p.K[0] * x + p.K[1] * y + p.K[2] * z;
+    const float pv = p.K[3] * x + p.K[4] * y + p.K[5] * z;
+    const float pw = p.K[6] * x + p.K[7] * y + p.K[8] * z;
+    const float u = pu / pw, v = pv / pw;
+    const bool valid_z = z > p.depth_eps;
+    const float logz = valid_z ? logf(z) : 0.0f;
+    const bool valid = (u > p.pixel_border) && (u < (float)(p.W - 1) - p.pixel_border) &&
+                       (v > p.pixel_border) && (v < (float)(p.H - 1) - p.pixel_border) && valid_z &&
+                       (r1.z != 0.0f);
+    const float vf = valid ? 1.0f : 0.0f;
+    const float si_p = vf * (p.c_a * sq), si_z = vf * (p.c_b * sq);
+    const float zi = 1.0f / z;
+    const float res[3] = {r0.w - u, r1.x - v, r1.y - logz};
+    float dh[3], J[7];
+    dh[0] = p.K[0] * zi;
+    dh[1] = 0.0f;
+    dh[2] = (-p.K[0] * x * zi) * zi;
+    chain_row(dh, Y, J);
+    acc_row(acc, J, res[0], si_p, p.huber_k);
+    dh[0] = 0.0f;
+    dh[1] = p.K[4] * zi;
+    dh[2] = (-p.K[4] * y * zi) * zi;
+    chain_row(dh, Y, J);
+    acc_row(acc, J, res[1], si_p, p.huber_k);
+    dh[0] = 0.0f;
+    dh[1] = 0.0f;
+    dh[2] = zi;
+    chain_row(dh, Y, J);
+    acc_row(acc, J, res[2], si_z, p.huber_k);
+  }
+}
+
+__global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackParams p) {
+  TrackState* st = a.state;
+  if (st->done) return;
+  if (track_skipped(st, p)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->status = M3S_TRACK_SKIPPED;
+      st->done = 1;
+    }
+    return;
+  }
+  const int iter0 = st->iter;
+  const double old_cost = st->old_cost;
+  if (blockIdx.x == 0) GN_STAMP(0);
+  float T[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) T[c] = st->T[c];
+  double acc[GN_NSUM];
+#pragma unroll
+  for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
+  const float4* rec = reinterpret_cast<const float4*>(a.rec);
+  const int stride = gridDim.x * GN_THREADS;
+  for (int n0 = blockIdx.x * GN_THREADS + threadIdx.x; n0 < p.N; n0 += GN_PPT * stride) {
+    float4 r0[GN_PPT], r1[GN_PPT];
+#pragma unroll
+    for (int u = 0; u < GN_PPT; u++) {
+      const int n = min(n0 + u * stride, p.N - 1);
+      r0[u] = rec[2 * (size_t)n];
+      r1[u] = rec[2 * (size_t)n + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < GN_PPT; u++)
+      if (n0 + u * stride < p.N) gn_point(p, T, r0[u], r1[u], acc);
+  }
+  if (blockIdx.x == 0) GN_STAMP(1);
+  __shared__ double s_all[GN_THREADS][GN_LDS_LD];
+  __shared__ double s_grp[7][GN_NSUM];
+  __shared__ double s_sum[GN_NSUM];
+  __shared__ int s_last;
+  block_sum36(acc, s_all, s_grp, s_sum);
+  __syncthreads();
+  if (blockIdx.x == 0) GN_STAMP(2);
+  // publish this block's partial write-through (sc1 agent-scope stores: no release fence needed),
+  // drain, then take a ticket (cdna guide §5 "In-launch split-K reduction")
+  gdouble* part = (gdouble*)a.partials;
+  if (threadIdx.x < GN_NSUM)
+    __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add((gint*)&st->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == (int)gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  GN_STAMP(3);
+  // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r as 16-B vectors in
+  // one round trip, then the same deterministic LDS reduction
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double v[GN_NSUM];
+  if ((int)threadIdx.x < (int)gridDim.x) {
+    const double2* row = reinterpret_cast<const double2*>(a.partials + (size_t)threadIdx.x * GN_PSTRIDE);
+#pragma unroll
+    for (int c = 0; c < GN_NSUM / 2; c++) {
+      const double2 t = row[c];
+      v[2 * c] = t.x;
+      v[2 * c + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < GN_NSUM; c++) v[c] = 0.0;
+  }
+  block_sum36(v, s_all, s_grp, s_sum);
+  __syncthreads();
+  GN_STAMP(4);
+  if (threadIdx.x == 0) {
+    gn_finish(st, p, s_sum, T, iter0, old_cost);
+#ifdef M3S_GN_STAMPS
+    if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
+    __hip_atomic_store((gint*)&st->arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+}
+
+// keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77); X_kf, C_kf in place.
 __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, float* __restrict__ Xkf_canon,
                                                    float* __restrict__ Ckf_sum, const float* __restrict__ Xkf,
                                                    const float* __restrict__ Ckf, int N) {
@@ -367,23 +482,6 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
 
 }  // namespace m3s
 
-namespace m3s {
-// state <- {T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf, n_unique = -1}
-__global__ void track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk) {
-  if (threadIdx.x != 0) return;
-  float Ti[8], Tf[8], Tk[8];
-  for (int c = 0; c < 8; c++) {
-    Tf[c] = T_WCf[c];
-    Tk[c] = T_WCk[c];
-    st->T_WCk[c] = Tk[c];
-  }
-  sim3_inv(Tk, Ti);
-  sim3_mul_norm(Ti, Tf, st->T);
-  st->old_cost = __builtin_inf();
-  st->n_unique = -1;
-}
-}  // namespace m3s
-
 extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_WCf, const float* T_WCk,
                                             hipStream_t s) {
   hipLaunchKernelGGL(m3s::track_init_kernel, dim3(1), dim3(64), 0, s, a->state, T_WCf, T_WCk);
@@ -392,15 +490,19 @@ extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_W
 
 extern "C" hipError_t m3s_launch_track_setup(const TrackArgs* a, const TrackParams* p, hipStream_t s) {
   hipLaunchKernelGGL(m3s::track_setup_kernel, dim3((p->N + 255) / 256), dim3(256), 0, s, *a, *p);
+  if (!p->direct) {
+    const int n16 = (p->N + 15) / 16;
+    const int blocks = (n16 + 255) / 256 < 256 ? (n16 + 255) / 256 : 256;
+    hipLaunchKernelGGL(m3s::track_count_kernel, dim3(blocks), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(a->flags), n16, a->state);
+  }
   return hipGetLastError();
 }
 
 extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackParams* p, int nparts, int iters,
                                              hipStream_t s) {
-  for (int i = 0; i < iters; i++) {
-    hipLaunchKernelGGL(m3s::gn_lin_kernel, dim3(nparts), dim3(256), 0, s, *a, *p);
-    hipLaunchKernelGGL(m3s::gn_solve_kernel, dim3(1), dim3(256), 0, s, *a, *p, nparts);
-  }
+  if (nparts < 1 || nparts > GN_THREADS) return hipErrorInvalidValue;  // the tail loads one partial per thread
+  for (int i = 0; i < iters; i++) hipLaunchKernelGGL(m3s::gn_iter_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
   return hipGetLastError();
 }
 
@@ -410,3 +512,10 @@ extern "C" hipError_t m3s_launch_fuse(const void* state, float* Xkf_canon, float
                      reinterpret_cast<const TrackState*>(state), Xkf_canon, Ckf_sum, Xkf, Ckf, N);
   return hipGetLastError();
 }
+
+#ifdef M3S_GN_STAMPS
+extern "C" int m3s_debug_gn_stamps(unsigned long long* out) {
+  (void)hipDeviceSynchronize();
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_gn_stamps), sizeof(unsigned long long) * 128) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -41,6 +41,22 @@ def mast3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
     return idx_i2j, valid_match_j, Xr[0], Cr[0], Qr[0], Xr[1], Cr[1], Qr[1]
 
 
+_K_CACHE = {}
+
+
+def _host_K(K):
+    """Host copy of the intrinsics, cached per tensor version: a device->host read every frame would
+    serialise the host against the matcher kernels still in flight."""
+    key = (K.data_ptr(), K._version, str(K.device))
+    Kh = _K_CACHE.get(key)
+    if Kh is None:
+        Kh = K.detach().float().cpu().reshape(-1).tolist()
+        if len(_K_CACHE) > 64:
+            _K_CACHE.clear()
+        _K_CACHE[key] = Kh
+    return Kh
+
+
 def _track_config(cfg, use_calib, img_size, K):
     tc = _lib.TrackConfig()
     tc.mode = 1 if use_calib else 0
@@ -48,7 +64,7 @@ def _track_config(cfg, use_calib, img_size, K):
     tc.C_conf, tc.Q_conf, tc.min_match_frac = float(cfg["C_conf"]), float(cfg["Q_conf"]), float(cfg["min_match_frac"])
     if use_calib:
         tc.sigma_a, tc.sigma_b = float(cfg["sigma_pixel"]), float(cfg["sigma_depth"])
-        Kh = K.detach().float().cpu().reshape(-1).tolist()
+        Kh = _host_K(K)
         for i in range(9):
             tc.K[i] = Kh[i]
     else:
@@ -164,6 +180,8 @@ class FrameTracker:
         _lib.check(lib.m3s_track(ctypes.byref(ins), ctypes.byref(tc), ctypes.byref(fz), int(self.first_chunk),
                                  _lib.ptr(T_out), ctypes.byref(res), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)))
         self.last_result = res
+        if not direct:  # next frame: enqueue as many GN launches as this one needed (+1) before reading back
+            self.first_chunk = max(2, min(int(tc.max_iters), res.iters + 1))
         return res, T_out
 
     # ------------------------------------------------------------------ reference method surface

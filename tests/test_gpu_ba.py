@@ -60,7 +60,9 @@ def test_gauss_newton_vs_oracle(golden, mode):
     T1, dx1 = _call(mode, g["Twc0"], Xs, g["Cs"], ii, jj, g["idx2"], g["valid2"], g["Q2"], g["K"], H, W, max_iter=1)
     T1r, dx1r, _ = O.gauss_newton(mode, g["Twc0"], Xs, g["Cs"][..., 0], ii, jj, g["idx2"], g["valid2"][..., 0],
                                   g["Q2"][..., 0], p, 1, 1e-8)
-    np.testing.assert_allclose(dx1, dx1r, rtol=0, atol=1e-4 * np.abs(dx1r).max())
+    # (first step from the perturbed start: |dx| ~ 0.4 with cond(H) ~ 1e4, so fp32 rounding of the
+    #  per-point rows shows at ~1e-4 of the step)
+    np.testing.assert_allclose(dx1, dx1r, rtol=0, atol=5e-4 * np.abs(dx1r).max())
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib"])
