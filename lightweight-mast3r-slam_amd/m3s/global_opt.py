@@ -13,12 +13,22 @@ from m3s.config import config
 from m3s.geometry import constrain_points_to_ray
 from m3s.matching import match
 from m3s.sim3 import Sim3
+from m3s.tracker import frame_img_size
 
 
 def mast3r_match_symmetric(model, kfs_i, kfs_j):
     """mast3r_utils.py:149-187 with the ViT decode behind ``model.symmetric_inference`` returning
     X (4,b,H,W,3), C (4,b,H,W), D (4,b,H,W,F), Q (4,b,H,W) ordered ii, ji, jj, ij."""
-    X, C, D, Q = model.symmetric_inference(kfs_i, kfs_j)
+    fn = getattr(model, "symmetric_inference", None)
+    if fn is not None:
+        X, C, D, Q = fn(kfs_i, kfs_j)
+    else:  # the real ViT: the reference's own batched decode (mast3r_utils.py:117-146), stock PyTorch-ROCm
+        from mast3r_slam.mast3r_utils import mast3r_decode_symmetric_batch
+
+        X, C, D, Q = mast3r_decode_symmetric_batch(
+            model, torch.cat([k.feat for k in kfs_i]), torch.cat([k.pos for k in kfs_i]),
+            torch.cat([k.feat for k in kfs_j]), torch.cat([k.pos for k in kfs_j]),
+            [k.img_true_shape for k in kfs_i], [k.img_true_shape for k in kfs_j])
     b = X.shape[1]
     X11 = torch.cat((X[0], X[2]), dim=0)
     X21 = torch.cat((X[1], X[3]), dim=0)
@@ -125,7 +135,7 @@ class FactorGraph:
         if unique_kf_idx.numel() <= pin:
             return
         Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
-        img_size = self.frames[0].img_size
+        img_size = frame_img_size(self.frames[0])
         Xs = constrain_points_to_ray(img_size, Xs, K)
         ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
         pose_data = T_WCs.data[:, 0, :]

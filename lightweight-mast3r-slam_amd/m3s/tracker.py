@@ -28,10 +28,22 @@ def huber(r, k=1.345):
     return torch.where(r_abs < k, unit, k / r_abs)
 
 
+def asymmetric_inference(model, frame_i, frame_j):
+    """X, C, D, Q (2b,H,W,·) of the pair. Models with ``asymmetric_inference`` (synthetic / replayed
+    pointmaps) answer directly; the real AsymmetricMASt3R goes through the reference's own ViT helper
+    (``mast3r_utils.py:190-217``, stock PyTorch-ROCm, outside this package's scope)."""
+    fn = getattr(model, "asymmetric_inference", None)
+    if fn is not None:
+        return fn(frame_i, frame_j)
+    from mast3r_slam.mast3r_utils import mast3r_asymmetric_inference
+
+    return mast3r_asymmetric_inference(model, frame_i, frame_j)
+
+
 def mast3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
     """mast3r_utils.py:220-242 with the ViT call behind ``model.asymmetric_inference`` (stock
     PyTorch-ROCm, out of scope); returns idx_i2j, valid_match_j, Xii, Cii, Qii, Xji, Cji, Qji."""
-    X, C, D, Q = model.asymmetric_inference(frame_i, frame_j)
+    X, C, D, Q = asymmetric_inference(model, frame_i, frame_j)
     b = X.shape[0] // 2
     h, w = X.shape[1:3]
     idx_i2j, valid_match_j = match(X[:b], X[b:], D[:b], D[b:], idx_1_to_2_init=idx_i2j_init)
@@ -55,6 +67,14 @@ def _host_K(K):
             _K_CACHE.clear()
         _K_CACHE[key] = Kh
     return Kh
+
+
+def frame_img_size(frame):
+    """(H, W): ``frame.img.shape[-2:]`` for a reference Frame (tracker.py:47), ``img_size`` for m3s.frame."""
+    size = getattr(frame, "img_size", None)
+    if size is None:
+        size = frame.img.shape[-2:]
+    return tuple(int(x) for x in size)
 
 
 def _track_config(cfg, use_calib, img_size, K):
@@ -100,10 +120,12 @@ class FrameTracker:
         frame.update_pointmap(Xff, Cff)
 
         use_calib = config["use_calib"]
-        img_size = frame.img_size
+        img_size = frame_img_size(frame)
         K = keyframe.K if use_calib else None
         cfg = self.cfg
-        fuse_fused = cfg["filtering_mode"] == "weighted_pointmap"
+        # weighted_pointmap on an initialised keyframe is fused on the device (frame.py:74-77); every
+        # other filtering mode / an empty keyframe goes through keyframe.update_pointmap
+        fuse_fused = cfg["filtering_mode"] == "weighted_pointmap" and keyframe.N > 0
 
         res, T_out = self._run_track(
             idx=idx_f2k, valid=valid_match_k, Xf=frame.X_canon, Cf=frame.C, Nf=frame.N, Qff=Qff,
