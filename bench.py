@@ -14,6 +14,7 @@ synthetic factor graph's edges over the ranks (strong scaling, one RCCL all-redu
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP-event spans inside the timed loop (no roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
@@ -99,7 +102,7 @@ def bench_tracking(args, rank, world, dev):
         step(i)
     iters = []
     lib.m3s_timing_reset()
-    lib.m3s_timing_enable(1)
+    lib.m3s_timing_enable(0 if args.no_kernel_timing else 1)
     sync_all(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -138,6 +141,22 @@ def roofline(kern, N, gn_iters_mean):
     if "refine_lin" in out:
         out["refine_lin"]["TFLOPs"] = refine_flops / (out["refine_lin"]["avg_us"] * 1e-6) / 1e12
     return out
+
+
+KERNEL_SYMBOL = {"prep_rays": "prep_rays_kernel", "proj_occlusion": "proj_occlusion_kernel",
+                 "refine_lin": "refine_tile_kernel", "track_setup": "track_setup_kernel", "gn_iters": "gn_iter_kernel"}
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch of `name` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, scripts/profile_summary.py); None if absent."""
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc.json")))
+    if not files:
+        return None
+    for k, v in json.load(open(files[-1])).items():
+        if KERNEL_SYMBOL.get(name, name) in k:
+            return v["traffic_bytes"]
+    return None
 
 
 def bench_ba(args, rank, world, dev):
@@ -228,14 +247,17 @@ def main():
     value = total_frames / elapsed
     rl = roofline(kern, N, gn_iters)
     log(f"[rank {rank}] kernels: {json.dumps(rl)}")
-    dom = max(rl.items(), key=lambda kv: kv[1]["avg_us"] * kern[kv[0]][1])
-    name, d = dom
-    if name == "refine_lin":
-        roof = {"kernel": name, "bound": "valu", "achieved": d["TFLOPs"], "peak": VALU_F32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": d["TFLOPs"] / VALU_F32_PEAK_TFLOPS, "traffic": None}
-    else:
-        roof = {"kernel": name, "bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": d["GBps"] / HBM_PEAK_GBS, "traffic": None}
+    roof = None
+    if rl:
+        name, d = max(rl.items(), key=lambda kv: kv[1]["avg_us"] * kern[kv[0]][1])
+        if name == "refine_lin":
+            roof = {"kernel": name, "bound": "valu", "achieved": d["TFLOPs"], "peak": VALU_F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": d["TFLOPs"] / VALU_F32_PEAK_TFLOPS}
+        else:
+            roof = {"kernel": name, "bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": d["GBps"] / HBM_PEAK_GBS}
+        roof["traffic"] = pmc_traffic(name)
+        roof["avg_us"] = d["avg_us"]
     ba = None
     if not args.no_ba:
         ba = bench_ba(args, rank, world, dev)

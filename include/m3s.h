@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define M3S_ABI_VERSION 1
+#define M3S_ABI_VERSION 2
 
 #define M3S_OK 0
 #define M3S_EINVAL -1  /* bad shape / argument (reference: TORCH_CHECK -> RuntimeError) */
@@ -152,10 +152,12 @@ typedef struct m3s_track_inputs {
 } m3s_track_inputs;
 
 typedef struct m3s_track_fuse_args {
-  float* Xk_canon;    /* (N,3) keyframe X_canon, updated in place; NULL = no fusion */
-  float* Ck_sum;      /* (N)   keyframe C, updated in place */
-  const float* Xkf;   /* (N,3) model output: keyframe points in the frame's camera */
-  const float* Ckf;   /* (N) */
+  const float* Xk_canon; /* (N,3) keyframe X_canon; NULL = no fusion */
+  const float* Ck_sum;   /* (N)   keyframe C */
+  const float* Xkf;      /* (N,3) model output: keyframe points in the frame's camera */
+  const float* Ckf;      /* (N) */
+  float* Xk_out;         /* (N,3) fused X_canon (may alias Xk_canon: in place) */
+  float* Ck_out;         /* (N)   fused C (may alias Ck_sum) */
 } m3s_track_fuse_args;
 
 typedef struct m3s_track_result {

@@ -27,9 +27,10 @@ hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int
 hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*, int, int, int, int, int, int,
                                  hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
-hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, hipStream_t);
-hipError_t m3s_launch_fuse(const void*, float*, float*, const float*, const float*, int, hipStream_t);
-hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, hipStream_t);
+hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
+hipError_t m3s_launch_fuse(const void*, int, const float*, const float*, float*, float*, const float*, const float*,
+                           int, hipStream_t);
+hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
 }
@@ -73,11 +74,25 @@ struct Carver {
   } while (0)
 
 // ---- per-kernel HIP-event timing (bench.py reads it; off by default, zero cost when off) ----
+// Events come from a pool that is created once and recycled by m3s_timing_reset: creating events
+// per launch costs host time inside the measured loop.
 struct TimedSpan {
   hipEvent_t a, b;
 };
 std::map<std::string, std::vector<TimedSpan>> g_spans;
+std::vector<hipEvent_t> g_event_pool;  // free events
 bool g_timing = false;
+
+hipEvent_t pool_event() {
+  if (g_event_pool.empty()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  hipEvent_t e = g_event_pool.back();
+  g_event_pool.pop_back();
+  return e;
+}
 
 struct Span {
   hipStream_t s;
@@ -85,7 +100,9 @@ struct Span {
   const char* name;
   Span(const char* n, hipStream_t st) : s(st), name(n) {
     if (!g_timing) return;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    a = pool_event();
+    b = pool_event();
+    if (a == nullptr || b == nullptr) {
       a = b = nullptr;
       return;
     }
@@ -100,13 +117,20 @@ struct Span {
 
 }  // namespace
 
-extern "C" void m3s_timing_enable(int on) { g_timing = on != 0; }
+extern "C" void m3s_timing_enable(int on) {
+  g_timing = on != 0;
+  while (g_timing && g_event_pool.size() < 1024) {  // pre-create outside any timed loop
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) break;
+    g_event_pool.push_back(e);
+  }
+}
 
 extern "C" void m3s_timing_reset(void) {
   for (auto& kv : g_spans)
     for (auto& sp : kv.second) {
-      (void)hipEventDestroy(sp.a);
-      (void)hipEventDestroy(sp.b);
+      g_event_pool.push_back(sp.a);
+      g_event_pool.push_back(sp.b);
     }
   g_spans.clear();
 }
@@ -225,6 +249,21 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
 // tracking
 // ------------------------------------------------------------------------------------------
 // GN blocks: 2 points per lane at 512x512 (512 blocks = 2 per CU), at most 512 partials to reduce
+// pinned host copy of the device state: the one per-frame readback is a direct DMA, not a staged copy
+static TrackState* pinned_state() {
+  static thread_local TrackState* h = nullptr;
+  if (h == nullptr) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(TrackState), hipHostMallocDefault) != hipSuccess) {
+      static thread_local TrackState fallback;  // pageable: still correct, slower copy
+      h = &fallback;
+    } else {
+      h = static_cast<TrackState*>(p);
+    }
+  }
+  return h;
+}
+
 static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
 
 static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, double** partials, float** rec) {
@@ -305,37 +344,35 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   p.cy = cfg->K[5];
   if (p.mode == 1) M3S_CHECK(p.fx != 0.0f && p.fy != 0.0f, "track: calib mode needs K");
   hipStream_t s = (hipStream_t)stream;
-  const size_t flag_bytes = ((size_t)N + 15) / 16 * 16;
-  HIP_TRY(hipMemsetAsync(st, 0, sizeof(TrackState), s), "track memset");
-  HIP_TRY(hipMemsetAsync(a.flags, 0, flag_bytes, s), "track memset");
-  HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, s), "track init launch");
+  a.T_out = T_out_dev;
+  const bool do_fuse = fuse && fuse->Xk_canon;
+  if (do_fuse) M3S_CHECK(fuse->Ck_sum && fuse->Xkf && fuse->Ckf, "track: fusion needs Ck_sum, Xkf, Ckf");
+  HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
   {
     Span sp("track_setup", s);
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
   }
   const int nparts = track_nparts(N);
-  int launched = 0;
+  int launched = 0, chunk_id = 0;
   int chunk = std::max(1, std::min(first_chunk, p.max_iters));
-  TrackState hs;
-  for (;;) {
+  TrackState& hs = *pinned_state();
+  for (;; chunk_id++) {
     {
       Span sp("gn_iters", s);
-      HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, chunk, s), "track iterate launch");
+      HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, chunk, chunk_id, s), "track iterate launch");
     }
     launched += chunk;
-    if (T_out_dev) {
-      HIP_TRY(hipMemcpyAsync(T_out_dev, st->T_WCf, 8 * sizeof(float), hipMemcpyDeviceToDevice, s), "track copy");
-      HIP_TRY(hipMemcpyAsync(T_out_dev + 8, st->T, 8 * sizeof(float), hipMemcpyDeviceToDevice, s), "track copy");
-    }
+    // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
+    // before the readback, it runs only if this batch finished the solve (done_chunk == chunk_id)
+    if (do_fuse)
+      HIP_TRY(m3s_launch_fuse(st, chunk_id, fuse->Xk_canon, fuse->Ck_sum, fuse->Xk_out ? fuse->Xk_out : (float*)fuse->Xk_canon,
+                              fuse->Ck_out ? fuse->Ck_out : (float*)fuse->Ck_sum, fuse->Xkf, fuse->Ckf, N, s),
+              "track fuse launch");
     HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
     HIP_TRY(hipStreamSynchronize(s), "track sync");
     if (hs.done || launched >= p.max_iters) break;
     chunk = std::min(8, p.max_iters - launched);
   }
-  // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) only after a successful solve (tracker.py:91-101);
-  // enqueued after the last readback, stream order makes it visible to every later consumer.
-  if (fuse && fuse->Xk_canon && (hs.status == M3S_TRACK_OK || hs.status == M3S_TRACK_MAX_ITERS))
-    HIP_TRY(m3s_launch_fuse(st, fuse->Xk_canon, fuse->Ck_sum, fuse->Xkf, fuse->Ckf, N, s), "track fuse launch");
   memcpy(result->T_WCf, hs.T_WCf, sizeof(result->T_WCf));
   memcpy(result->T_CkCf, hs.T, sizeof(result->T_CkCf));
   result->cost = hs.last_cost;

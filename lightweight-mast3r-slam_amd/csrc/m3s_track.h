@@ -21,8 +21,8 @@ struct TrackState {
   int n_valid_opt;
   int n_valid_kf;
   int n_unique;
-  int arrive;  // per-iteration block-arrival ticket of the fused GN kernel (last arriver solves)
-  int pad;
+  int arrive;      // per-iteration block-arrival ticket of the fused GN kernel (last arriver solves)
+  int done_chunk;  // host chunk id of the GN launch batch that finished (gates the fuse launch)
 };
 
 struct TrackParams {
@@ -53,4 +53,5 @@ struct TrackArgs {
   uint8_t* flags;              // (N, padded to 16) unique(idx[valid]) byte map (workspace, zeroed per frame)
   double* partials;            // (nparts, 40) block partial sums (workspace)
   TrackState* state;
+  float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
 };

@@ -10,15 +10,16 @@
 //   keyframe fusion + selection stats  tracker.py:95-114, frame.py:41-77 (weighted_pointmap)
 //
 // Device pipeline per frame, no host synchronisation inside:
-//   track_init   : T_CkCf = T_WCk^-1 T_WCf into the device state
+//   track_init   : zero the state and the unique(idx[valid]) byte map, T_CkCf = T_WCk^-1 T_WCf
 //   track_setup  : gather Xf[idx], Qk = sqrt(Qff[idx] Qkf), validity masks, a 32-byte per-point GN
-//                  record, counts (valid_opt, valid_kf) and the unique(idx[valid]) byte map
-//   track_count  : popcount of the byte map (torch.unique(...).shape[0], tracker.py:106-108)
+//                  record, counts (valid_opt, valid_kf) and the byte map
 //   gn_iter (xI) : ONE launch per GN iteration: every block accumulates the 28 (H upper) + 7 (g)
 //                  + 1 (cost) sums in fp64, publishes them write-through (sc1) and takes an arrival
 //                  ticket; the last-arriving block reduces all partials, solves the 7x7 system in
 //                  fp64, retracts T <- Exp(tau) T, applies the convergence test and, once done,
-//                  writes T_WCf = T_WCk T_CkCf. Later launches exit at their first load.
+//                  writes T_WCf = T_WCk T_CkCf (also to the caller's T_out). Later launches exit at
+//                  their first load. The first launch also popcounts the byte map
+//                  (torch.unique(...).shape[0], tracker.py:106-108).
 //   fuse         : keyframe X <- (C X + C' T_CkCf Xkf) / (C + C'), C += C'
 #include "m3s_common.hpp"
 #include "m3s_track.h"
@@ -60,9 +61,14 @@ __device__ __forceinline__ void sim3_inv(const float* A, float* C) {
   C[7] = si;
 }
 
-// state <- {T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}
-__global__ void track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk) {
-  if (threadIdx.x != 0) return;
+// state <- {0, T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}; the grid zeroes
+// the unique-idx byte map (replaces two memsets + a one-lane launch)
+__global__ void __launch_bounds__(256) track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk,
+                                                         uint4* flags, int n16) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) flags[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i != 0) return;
+  *st = TrackState{};
   float Ti[8], Tf[8], Tk[8];
   for (int c = 0; c < 8; c++) {
     Tf[c] = T_WCf[c];
@@ -106,7 +112,7 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
     const bool valid_opt = vm && (cf > p.C_conf) && (ck > p.C_conf) && (qk > p.Q_conf);
     v_opt = valid_opt;
     v_kf = vm && (qk > p.Q_conf);
-    if (vm) a.flags[i] = 1;  // benign same-value races; counted by track_count_kernel
+    if (vm) a.flags[i] = 1;  // benign same-value races; popcounted by the first GN launch
     const float sq = valid_opt ? sqrtf(qk) : 0.0f;
     float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
     const float* Xf = a.Xf + i * 3;
@@ -141,21 +147,6 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
     atomicAdd(&a.state->n_valid_opt, s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3]);
     atomicAdd(&a.state->n_valid_kf, s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3]);
   }
-}
-
-// number of distinct idx among valid matches = nonzero bytes of the flag map (16 bytes per lane-load)
-__global__ void __launch_bounds__(256) track_count_kernel(const uint4* __restrict__ flags, int n16,
-                                                          TrackState* __restrict__ st) {
-  int cnt = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
-    const uint4 v = flags[i];
-    cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // flags are 0/1 bytes
-  }
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-  __shared__ int s[4];
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&st->n_unique, s[0] + s[1] + s[2] + s[3]);
 }
 
 __device__ __forceinline__ bool track_skipped(const TrackState* st, const TrackParams& p) {
@@ -232,7 +223,7 @@ __device__ bool chol7(const double Hd[7][7], const double gd[7], double tau[7]) 
 // one thread: H, g, cost -> tau -> T update + convergence (tracker.py:156-171, 186-209).
 // T, iter and old_cost come in registers (loaded at kernel start, not re-read on the serial tail).
 __device__ void gn_finish(TrackState* st, const TrackParams& p, const double* sum, const float* T, int iter,
-                          double old) {
+                          double old, float* T_out, int chunk_id) {
   double H[7][7], g[7], tau[7];
   int l = 0;
   for (int c = 0; c < 7; c++)
@@ -247,6 +238,7 @@ __device__ void gn_finish(TrackState* st, const TrackParams& p, const double* su
   if (!chol7(H, g, tau)) {
     st->status = M3S_TRACK_CHOLESKY_FAILED;
     st->done = 1;
+    st->done_chunk = chunk_id;
     return;
   }
   float tf[7];
@@ -267,9 +259,16 @@ __device__ void gn_finish(TrackState* st, const TrackParams& p, const double* su
   if (conv || it >= p.max_iters) {
     st->status = conv ? M3S_TRACK_OK : M3S_TRACK_MAX_ITERS;
     st->done = 1;
-    float Tk[8];
+    st->done_chunk = chunk_id;
+    float Tk[8], Tw[8];
     for (int c = 0; c < 8; c++) Tk[c] = st->T_WCk[c];
-    sim3_mul_norm(Tk, Tn, st->T_WCf);  // T_WCf = T_WCk * T_CkCf
+    sim3_mul_norm(Tk, Tn, Tw);  // T_WCf = T_WCk * T_CkCf
+    for (int c = 0; c < 8; c++) st->T_WCf[c] = Tw[c];
+    if (T_out != nullptr)
+      for (int c = 0; c < 8; c++) {
+        T_out[c] = Tw[c];
+        T_out[8 + c] = Tn[c];
+      }
   }
 }
 
@@ -376,7 +375,7 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
   }
 }
 
-__global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackParams p) {
+__global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackParams p, int chunk_id) {
   TrackState* st = a.state;
   if (st->done) return;
   if (track_skipped(st, p)) {
@@ -388,6 +387,19 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
   }
   const int iter0 = st->iter;
   const double old_cost = st->old_cost;
+  if (iter0 == 0 && !p.direct) {
+    // first iteration also counts unique(idx[valid]) (tracker.py:106-108): popcount of the byte map
+    // written by track_setup (flags are 0/1 bytes), one atomic per wave
+    const uint4* fl = reinterpret_cast<const uint4*>(a.flags);
+    const int n16 = (p.N + 15) / 16;
+    int cnt = 0;
+    for (int i = blockIdx.x * GN_THREADS + threadIdx.x; i < n16; i += gridDim.x * GN_THREADS) {
+      const uint4 v = fl[i];
+      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    }
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&st->n_unique, cnt);
+  }
   if (blockIdx.x == 0) GN_STAMP(0);
   float T[8];
 #pragma unroll
@@ -452,7 +464,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
   __syncthreads();
   GN_STAMP(4);
   if (threadIdx.x == 0) {
-    gn_finish(st, p, s_sum, T, iter0, old_cost);
+    gn_finish(st, p, s_sum, T, iter0, old_cost, a.T_out, chunk_id);
 #ifdef M3S_GN_STAMPS
     if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -460,11 +472,16 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
   }
 }
 
-// keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77); X_kf, C_kf in place.
-__global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, float* __restrict__ Xkf_canon,
-                                                   float* __restrict__ Ckf_sum, const float* __restrict__ Xkf,
-                                                   const float* __restrict__ Ckf, int N) {
-  if (!(st->done && (st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS))) return;
+// keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77). Runs only if the
+// GN batch `chunk_id` finished with a pose (so it can be enqueued before the host reads the state
+// back). Out of place like the reference (new X_canon / C tensors); X_out may alias X_in.
+__global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id,
+                                                   const float* X_in, const float* C_in, float* X_out, float* C_out,
+                                                   const float* __restrict__ Xkf, const float* __restrict__ Ckf,
+                                                   int N) {
+  if (!(st->done && st->done_chunk == chunk_id &&
+        (st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)))
+    return;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float T[8];
@@ -473,43 +490,44 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
   const float X[3] = {Xkf[3 * (size_t)n], Xkf[3 * (size_t)n + 1], Xkf[3 * (size_t)n + 2]};
   float Y[3];
   actSim3(T, X, Y);
-  const float c0 = Ckf_sum[n], c1 = Ckf[n];
+  const float c0 = C_in[n], c1 = Ckf[n];
   const float den = c0 + c1;
+  float Xo[3];
 #pragma unroll
-  for (int k = 0; k < 3; k++) Xkf_canon[3 * (size_t)n + k] = (c0 * Xkf_canon[3 * (size_t)n + k] + c1 * Y[k]) / den;
-  Ckf_sum[n] = den;
+  for (int k = 0; k < 3; k++) Xo[k] = (c0 * X_in[3 * (size_t)n + k] + c1 * Y[k]) / den;
+#pragma unroll
+  for (int k = 0; k < 3; k++) X_out[3 * (size_t)n + k] = Xo[k];
+  C_out[n] = den;
 }
 
 }  // namespace m3s
 
-extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_WCf, const float* T_WCk,
+extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_WCf, const float* T_WCk, int N,
                                             hipStream_t s) {
-  hipLaunchKernelGGL(m3s::track_init_kernel, dim3(1), dim3(64), 0, s, a->state, T_WCf, T_WCk);
+  const int n16 = (N + 15) / 16;  // the byte map is carved with a 16-B padded length
+  hipLaunchKernelGGL(m3s::track_init_kernel, dim3((n16 + 255) / 256), dim3(256), 0, s, a->state, T_WCf, T_WCk,
+                     reinterpret_cast<uint4*>(a->flags), n16);
   return hipGetLastError();
 }
 
 extern "C" hipError_t m3s_launch_track_setup(const TrackArgs* a, const TrackParams* p, hipStream_t s) {
   hipLaunchKernelGGL(m3s::track_setup_kernel, dim3((p->N + 255) / 256), dim3(256), 0, s, *a, *p);
-  if (!p->direct) {
-    const int n16 = (p->N + 15) / 16;
-    const int blocks = (n16 + 255) / 256 < 256 ? (n16 + 255) / 256 : 256;
-    hipLaunchKernelGGL(m3s::track_count_kernel, dim3(blocks), dim3(256), 0, s,
-                       reinterpret_cast<const uint4*>(a->flags), n16, a->state);
-  }
   return hipGetLastError();
 }
 
 extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackParams* p, int nparts, int iters,
-                                             hipStream_t s) {
+                                             int chunk_id, hipStream_t s) {
   if (nparts < 1 || nparts > GN_THREADS) return hipErrorInvalidValue;  // the tail loads one partial per thread
-  for (int i = 0; i < iters; i++) hipLaunchKernelGGL(m3s::gn_iter_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
+  for (int i = 0; i < iters; i++)
+    hipLaunchKernelGGL(m3s::gn_iter_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p, chunk_id);
   return hipGetLastError();
 }
 
-extern "C" hipError_t m3s_launch_fuse(const void* state, float* Xkf_canon, float* Ckf_sum, const float* Xkf,
-                                      const float* Ckf, int N, hipStream_t s) {
+extern "C" hipError_t m3s_launch_fuse(const void* state, int chunk_id, const float* X_in, const float* C_in,
+                                      float* X_out, float* C_out, const float* Xkf, const float* Ckf, int N,
+                                      hipStream_t s) {
   hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s,
-                     reinterpret_cast<const TrackState*>(state), Xkf_canon, Ckf_sum, Xkf, Ckf, N);
+                     reinterpret_cast<const TrackState*>(state), chunk_id, X_in, C_in, X_out, C_out, Xkf, Ckf, N);
   return hipGetLastError();
 }
 

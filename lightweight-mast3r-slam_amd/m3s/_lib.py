@@ -14,6 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # M3S_LIB: alternative build of the same library (kernel experiments); still the HIP library, no fallback
 LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libm3s.so")
 
+ABI_VERSION = 2  # include/m3s.h M3S_ABI_VERSION
+
 c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
 
 
@@ -42,7 +44,8 @@ class TrackInputs(ctypes.Structure):
 
 
 class TrackFuse(ctypes.Structure):
-    _fields_ = [("Xk_canon", c_void_p), ("Ck_sum", c_void_p), ("Xkf", c_void_p), ("Ckf", c_void_p)]
+    _fields_ = [("Xk_canon", c_void_p), ("Ck_sum", c_void_p), ("Xkf", c_void_p), ("Ckf", c_void_p),
+                ("Xk_out", c_void_p), ("Ck_out", c_void_p)]
 
 
 class TrackResult(ctypes.Structure):
@@ -98,8 +101,8 @@ def load(require_gpu=True):
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
-        if lib.m3s_abi_version() != 1:
-            raise RuntimeError("m3s: ABI version mismatch")
+        if lib.m3s_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"m3s: ABI version mismatch (library {lib.m3s_abi_version()}, bindings {ABI_VERSION})")
         _LIB = lib
     return _LIB
 

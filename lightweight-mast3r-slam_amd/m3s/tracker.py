@@ -140,9 +140,11 @@ class FrameTracker:
             print(f"Cholesky failed {frame.frame_id}")
             return False, [], True
 
-        frame.T_WC = Sim3(T_out[:8].view(1, 8).clone())
-        T_CkCf = Sim3(T_out[8:].view(1, 8).clone())
-        if fuse_fused:  # X/C fused in place on the device by m3s_track (frame.py:74-77)
+        # T_out is a fresh (16,) tensor per call, so views need no copy
+        frame.T_WC = Sim3(T_out[:8].view(1, 8))
+        T_CkCf = Sim3(T_out[8:].view(1, 8))
+        if fuse_fused:  # X/C fused on the device by m3s_track into new tensors (frame.py:74-77)
+            keyframe.X_canon, keyframe.C = self._fused
             keyframe.N += 1
             keyframe.N_updates += 1
         else:
@@ -187,15 +189,16 @@ class FrameTracker:
             valid_meas_k=_lib.ptr(valid_meas_k).value)
         fz = _lib.TrackFuse()
         keep = []
-        if fuse is not None:
+        self._fused = None
+        if fuse is not None:  # out of place like frame.py:75-76 (earlier holders keep the old tensors)
             kf, Xkf, Ckf = fuse
-            if not (kf.X_canon.is_contiguous() and kf.C.is_contiguous() and kf.X_canon.dtype == torch.float32):
-                kf.X_canon = kf.X_canon.float().contiguous()
-                kf.C = kf.C.float().contiguous()
+            Xin, Cin = c(kf.X_canon), c(kf.C)
             Xkf_c, Ckf_c = c(Xkf), c(Ckf)
-            keep += [Xkf_c, Ckf_c]
-            fz = _lib.TrackFuse(Xk_canon=_lib.ptr(kf.X_canon).value, Ck_sum=_lib.ptr(kf.C).value,
-                                Xkf=_lib.ptr(Xkf_c).value, Ckf=_lib.ptr(Ckf_c).value)
+            Xo, Co = torch.empty_like(Xin), torch.empty_like(Cin)
+            keep += [Xin, Cin, Xkf_c, Ckf_c]
+            self._fused = (Xo, Co)
+            fz = _lib.TrackFuse(Xk_canon=_lib.ptr(Xin).value, Ck_sum=_lib.ptr(Cin).value, Xkf=_lib.ptr(Xkf_c).value,
+                                Ckf=_lib.ptr(Ckf_c).value, Xk_out=_lib.ptr(Xo).value, Ck_out=_lib.ptr(Co).value)
         T_out = torch.empty(16, dtype=torch.float32, device=dev)
         res = _lib.TrackResult()
         ws = _lib.workspace("track", lib.m3s_track_workspace_size(N), dev)
@@ -246,7 +249,7 @@ class FrameTracker:
                                      img_size=img_size, K=K, direct=True, meas_k=meas_k, valid_meas_k=valid_meas_k)
         if res.status == _lib.TRACK_CHOLESKY_FAILED:
             raise RuntimeError("linalg.cholesky: The factorization could not be completed")
-        return Sim3(T_out[:8].view(1, 8).clone()), Sim3(T_out[8:].view(1, 8).clone())
+        return Sim3(T_out[:8].view(1, 8)), Sim3(T_out[8:].view(1, 8))
 
     def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
         """tracker.py:173-214 -> (T_WCf, T_CkCf)."""

@@ -23,7 +23,8 @@ def test_abi_library_exports_every_declared_symbol():
     assert not missing, missing
     assert declared == set(_lib.EXPORTED)  # the ctypes table binds exactly the header
     lib.m3s_abi_version.restype = ctypes.c_int
-    assert lib.m3s_abi_version() == 1
+    hdr_version = int(re.search(r"#define M3S_ABI_VERSION (\d+)", header).group(1))
+    assert lib.m3s_abi_version() == hdr_version == _lib.ABI_VERSION
 
 
 def test_workspace_sizes_are_monotone():
