@@ -19,13 +19,13 @@ hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, 
 hipError_t m3s_launch_iter_proj(const float*, const float*, const float*, float*, uint8_t*, int, int, int, int, int,
                                 float, float, hipStream_t);
 hipError_t m3s_launch_proj_occlusion(const float*, const float*, const float*, const int64_t*, int*, uint8_t*, int, int,
-                                     int, int, float, float, float, hipStream_t);
+                                     int, int, float, float, float, int*, hipStream_t);
 hipError_t m3s_launch_refine_f16(const void*, const void*, const int64_t*, int64_t*, int, int, int, int, int, int, int,
                                  hipStream_t);
 hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int64_t*, int, int, int, int, int, int,
                                  int, hipStream_t);
 hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*, int, int, int, int, int, int,
-                                 hipStream_t);
+                                 void*, int*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
 hipError_t m3s_launch_fuse(const void*, int, const float*, const float*, float*, float*, const float*, const float*,
@@ -195,19 +195,27 @@ extern "C" int m3s_refine_matches(int dtype, const void* D11, const void* D21, c
 // ------------------------------------------------------------------------------------------
 // fused match
 // ------------------------------------------------------------------------------------------
-static size_t match_carve(Carver& c, int B, int H, int W, int F, float** rays9, void** D11h, int** p1) {
-  *rays9 = c.take<float>((size_t)B * H * W * 9);
-  *D11h = c.take<uint16_t>((size_t)B * H * W * F);
-  *p1 = c.take<int>((size_t)B * H * W * 2);
+struct MatchWs {
+  float* rays9;   // (B,H,W,9) rays + gradients
+  void* D11h;     // (B,H,W,F) f16
+  int* p1;        // (B,N,2) int32
+  int4* olist;    // (B*N) refine deferred-outlier records
+  int* ocount;    // refine deferred-outlier count
+};
+
+static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
+  w->rays9 = c.take<float>((size_t)B * H * W * 9);
+  w->D11h = c.take<uint16_t>((size_t)B * H * W * F);
+  w->p1 = c.take<int>((size_t)B * H * W * 2);
+  w->olist = c.take<int4>((size_t)B * H * W);
+  w->ocount = c.take<int>(1);
   return c.off;
 }
 
 extern "C" size_t m3s_match_workspace_size(int B, int H, int W, int F) {
   Carver c(nullptr);
-  float* r;
-  void* d;
-  int* p;
-  return match_carve(c, B, H, W, F, &r, &d, &p);
+  MatchWs w;
+  return match_carve(c, B, H, W, F, &w);
 }
 
 extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, const float* D21,
@@ -220,10 +228,11 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   M3S_CHECK(max_iter >= 0 && radius >= 0 && dilation_max >= 0, "match: negative parameter");
   if (workspace_bytes < m3s_match_workspace_size(B, H, W, F)) return fail(M3S_ESPACE, "match: workspace too small");
   Carver c(workspace);
-  float* rays9;
-  void* D11h;
-  int* p1;
-  match_carve(c, B, H, W, F, &rays9, &D11h, &p1);
+  MatchWs w;
+  match_carve(c, B, H, W, F, &w);
+  float* rays9 = w.rays9;
+  void* D11h = w.D11h;
+  int* p1 = w.p1;
   hipStream_t s = (hipStream_t)stream;
   {
     Span sp("prep_rays", s);
@@ -232,14 +241,15 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   {
     Span sp("proj_occlusion", s);
     HIP_TRY(m3s_launch_proj_occlusion(rays9, X11, X21, idx_init, p1, valid_out, B, H, W, max_iter, lambda_init,
-                                      cost_thresh, dist_thresh, s),
+                                      cost_thresh, dist_thresh, w.ocount, s),
             "match proj launch");
   }
   // radius == 0: the refine loop is empty and the kernel only writes idx = pixel_to_lin(p1)
   // (matching.py:78-88); D11h is never read then.
   {
     Span sp("refine_lin", s);
-    HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, s),
+    HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, w.olist,
+                                  w.ocount, s),
             "match refine launch");
   }
   return M3S_OK;

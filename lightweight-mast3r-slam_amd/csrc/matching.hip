@@ -13,7 +13,7 @@
 #include "m3s_half.hpp"
 
 extern "C" hipError_t m3s_launch_refine_tile(const void*, const void*, const void*, void*, int, int, int, int, int,
-                                             int, int, hipStream_t);
+                                             int, int, void*, int*, hipStream_t);
 
 namespace m3s {
 
@@ -177,10 +177,11 @@ __global__ void __launch_bounds__(256) iter_proj_kernel(const float* __restrict_
 __global__ void __launch_bounds__(256) proj_occlusion_kernel(
     const float* __restrict__ rays, const float* __restrict__ X11, const float* __restrict__ X21,
     const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
-    int max_iter, float lambda_init, float cost_thresh, float dist_thresh) {
+    int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter) {
   const int N = H * W;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
+  if (zero_counter != nullptr && n == 0 && b == 0) *zero_counter = 0;  // refine's outlier list (next launch)
   if (n >= N) return;
   const size_t bn = (size_t)b * N + n;
   const float x = X21[bn * 3 + 0], y = X21[bn * 3 + 1], z = X21[bn * 3 + 2];
@@ -354,10 +355,10 @@ extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, 
 extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* X11, const float* X21,
                                                 const int64_t* idx_init, int* p1, uint8_t* valid, int B, int H, int W,
                                                 int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-                                                hipStream_t s) {
+                                                int* zero_counter, hipStream_t s) {
   dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
-                     max_iter, lambda_init, cost_thresh, dist_thresh);
+                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter);
   return hipGetLastError();
 }
 
@@ -366,8 +367,9 @@ extern "C" hipError_t m3s_launch_refine_f16(const void* D11, const void* D21, co
   dim3 grid((N + 255) / 256, B);
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11);
   const m3s::h1* q = reinterpret_cast<const m3s::h1*>(D21);
-  if (N == H * W && m3s_launch_refine_tile(D11, D21, p1, p1_new, B, H, W, F, radius, dilation_max, 0, s) ==
-                        hipSuccess)
+  if (N == H * W &&
+      m3s_launch_refine_tile(D11, D21, p1, p1_new, B, H, W, F, radius, dilation_max, 0, nullptr, nullptr, s) ==
+          hipSuccess)
     return hipSuccess;  // tiled LDS path (query n is pixel n of the grid)
   switch (F) {
     case 24:
@@ -397,11 +399,15 @@ extern "C" hipError_t m3s_launch_refine_f32(const float* D11, const float* D21, 
   return hipGetLastError();
 }
 
+// olist/ocount: deferred-outlier list (B*H*W int4) + counter, zeroed by proj_occlusion_kernel
 extern "C" hipError_t m3s_launch_refine_lin(const void* D11h, const float* D21, const int* p1, int64_t* idx_out, int B,
-                                            int H, int W, int F, int radius, int dilation_max, hipStream_t s) {
+                                            int H, int W, int F, int radius, int dilation_max, void* olist,
+                                            int* ocount, hipStream_t s) {
   dim3 grid((H * W + 255) / 256, B);
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
-  if (radius > 0 && m3s_launch_refine_tile(D11h, D21, p1, idx_out, B, H, W, F, radius, dilation_max, 1, s) == hipSuccess)
+  if (radius > 0 &&
+      m3s_launch_refine_tile(D11h, D21, p1, idx_out, B, H, W, F, radius, dilation_max, 1, olist, ocount, s) ==
+          hipSuccess)
     return hipSuccess;  // tiled LDS path
   switch (F) {
     case 24:

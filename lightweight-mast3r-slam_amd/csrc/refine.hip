@@ -11,13 +11,17 @@
 //     the centres within 16 px of it, places a 64-column x 40-row window over bbox +- 3d and streams
 //     D11 (f16) into LDS in three 8-channel chunks (16 B / px) with global_load_lds — one
 //     wave-instruction per window row. Four resident blocks per CU hide each other's fill latency
-//     (measured faster than double-buffering at two blocks per CU: RT_NBUF).
+//     (measured: faster than double-buffering at two blocks per CU).
 //   * Levels are specialised on d, so every candidate read is one ds_read_b128 with an immediate
 //     offset from a single per-lane base; the 49 running half sums live in registers across the
 //     three chunks (the sum stays sequential over k = 0..23: c10::Half step rounding unchanged).
-//   * Lanes whose 49 candidates do not all fall inside the window (outlier centres, a clipped
-//     window) are scored cooperatively by their wave straight from global memory: 49 lanes, one
-//     candidate each, then a first-maximum wave arg-max (same result as the sequential scan).
+//   * A lane whose 49 candidates do not fit the window (an outlier centre, a clipped window) is
+//     DEFERRED: its state (pixel, centre, running max, level) is appended to a list and the lane
+//     leaves the tile (it no longer widens the window of later levels). refine_outlier_kernel then
+//     finishes every deferred pixel with one wave per pixel: 49 lanes score the 49 candidates from
+//     global memory (all loads in flight at once) and a first-maximum wave arg-max reproduces the
+//     sequential strict-'>' scan (the running max only grows from +0). Without a list (reference
+//     op path, no workspace) the wave scores its outliers in place, one at a time (wave_level).
 //   * Tiles are dealt to XCDs in contiguous runs (bijective remap) so each XCD's 4 MiB L2 holds
 //     its slab of D11.
 // Compiled with -ffp-contract=off.
@@ -28,10 +32,7 @@ namespace m3s {
 #define RT_TW 32
 #define RT_TH 8
 #define RT_COLS 64
-#define RT_ROWS 40
-#ifndef RT_NBUF
-#define RT_NBUF 1  // 1: 40 KiB, 4 blocks/CU (measured faster); 2: 80 KiB, double-buffered chunks, 2 blocks/CU
-#endif
+#define RT_ROWS 40  // 40 x 64 x 16 B = 40 KiB per block: four blocks per CU
 
 typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
@@ -41,58 +42,40 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {  // bijective (cdna gu
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// Lanes whose level does not fit the window: the wave takes them one at a time, 49 lanes score the
-// 49 candidates of that pixel from global memory (three 16-B loads each, all in flight at once) and
-// a wave arg-max picks the first candidate in scan order holding the maximum -- the same result as
-// the reference's sequential strict-'>' scan, since the running max only grows from +0.
-#ifdef M3S_COOP_NOINLINE
-#define M3S_COOP_ATTR __attribute__((noinline))
-#else
-#define M3S_COOP_ATTR __forceinline__  // a call would spill the caller's live VGPRs to scratch
+#ifdef M3S_REFINE_STATS  // (experiment builds only) per-level deferred lanes / waves
+__device__ unsigned long long g_refine_stats[32];
 #endif
+
+// One level of one pixel by the whole wave (cu, cv, max_score, sq wave-uniform): lane c < 49 scores
+// candidate (c / 7, c % 7) from global memory; the first candidate in scan order holding the wave
+// maximum wins if it beats the running max — the sequential strict-'>' scan's result.
 template <int D>
-__device__ M3S_COOP_ATTR void refine_level_coop(const h1* __restrict__ img, int H, int W, const h2* q,
-                                                             int& cu, int& cv, h1& max_score, bool need, int lane) {
+__device__ __forceinline__ void wave_level(const h1* __restrict__ img, int H, int W, const h2* sq, int& cu, int& cv,
+                                           h1& max_score, int lane) {
   constexpr int R = 3, RD = R * D, F = 24, G = 2 * R + 1;
-  uint64_t m = __ballot(need);
   const int ci = lane / G, cj = lane % G;
-  while (m) {
-    const int src = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    const int scu = __shfl(cu, src, 64), scv = __shfl(cv, src, 64);
-    h2 sq[F / 2];
+  const int u = cu - RD + ci * D, v = cv - RD + cj * D;
+  const bool ok = lane < G * G && u >= 0 && u < W && v >= 0 && v < H;
+  const uint4* p =
+      reinterpret_cast<const uint4*>(img + ((size_t)min(max(v, 0), H - 1) * W + min(max(u, 0), W - 1)) * F);
+  const uint4 c0 = p[0], c1 = p[1], c2 = p[2];
+  h1 sc = (h1)0.0f;
+  add8(sc, &sq[0], c0);
+  add8(sc, &sq[4], c1);
+  add8(sc, &sq[8], c2);
+  const float sf = (ok && sc == sc) ? (float)sc : -INFINITY;  // NaN never wins a strict '>'
+  float vmax = sf;
 #pragma unroll
-    for (int k = 0; k < F / 2; k++) {
-      const int t = __shfl(*reinterpret_cast<const int*>(&q[k]), src, 64);
-      sq[k] = *reinterpret_cast<const h2*>(&t);
-    }
-    const int u = scu - RD + ci * D, v = scv - RD + cj * D;
-    const bool ok = lane < G * G && u >= 0 && u < W && v >= 0 && v < H;
-    const uint4* p = reinterpret_cast<const uint4*>(img + ((size_t)min(max(v, 0), H - 1) * W + min(max(u, 0), W - 1)) * F);
-    const uint4 c0 = p[0], c1 = p[1], c2 = p[2];
-    h1 sc = (h1)0.0f;
-    add8(sc, &sq[0], c0);
-    add8(sc, &sq[4], c1);
-    add8(sc, &sq[8], c2);
-    const float sf = (ok && sc == sc) ? (float)sc : -INFINITY;  // NaN never wins a strict '>'
-    float vmax = sf;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
-    const uint64_t hit = __ballot(sf == vmax);
-    const int first = __ffsll((long long)hit) - 1;
-    if (lane == src && vmax > (float)max_score) {
-      max_score = (h1)vmax;
-      cu = scu - RD + (first / G) * D;
-      cv = scv - RD + (first % G) * D;
-    }
+  for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+  const int first = __ffsll((long long)__ballot(sf == vmax)) - 1;
+  if (vmax > (float)max_score) {
+    max_score = (h1)vmax;
+    cu = cu - RD + (first / G) * D;
+    cv = cv - RD + (first % G) * D;
   }
 }
 
 // 49 candidates x one 8-channel chunk from the LDS window; base = candidate (0,0) of this lane
-#ifdef M3S_REFINE_STATS
-__device__ unsigned long long g_refine_stats[32];
-#endif
-
 template <int D>
 __device__ __forceinline__ void score_chunk(const uint4* base, const h2* q4, h1* s) {
   constexpr int G = 7;
@@ -105,13 +88,21 @@ __device__ __forceinline__ void score_chunk(const uint4* base, const h2* q4, h1*
   }
 }
 
+struct TileCtx {
+  const h1* img;
+  int H, W, lane, wid, u_pix, v_pix;
+  int bn;       // batch * N + pixel
+  int4* olist;  // deferred-pixel list (nullable: score outliers in place)
+  int* ocount;
+};
+
 template <int D>
-__device__ __forceinline__ void refine_level(const h1* __restrict__ img, int H, int W, bool active, const h2* q,
-                                             int& cu, int& cv, h1& max_score, uint4 (*lds)[RT_ROWS * RT_COLS],
-                                             int (*s_red)[4], int lane, int wid, int u_pix, int v_pix) {
+__device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, const h2* q, int& cu, int& cv,
+                                             h1& max_score, uint4* lds, int (*s_red)[4]) {
   constexpr int R = 3, G = 2 * R + 1, F = 24, RD = R * D;
+  const int lane = t.lane, wid = t.wid, H = t.H, W = t.W;
   // 1) tile flow estimate: mean centre displacement (cu - u_pix) over active lanes
-  int su = active ? cu - u_pix : 0, sv = active ? cv - v_pix : 0, na = active ? 1 : 0;
+  int su = active ? cu - t.u_pix : 0, sv = active ? cv - t.v_pix : 0, na = active ? 1 : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     su += __shfl_xor(su, off, 64);
@@ -128,8 +119,8 @@ __device__ __forceinline__ void refine_level(const h1* __restrict__ img, int H, 
   const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
   const int fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
   const int fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
-  // 2) bbox of the inlier centres (within 16 px of pixel + tile flow); outliers take the global path
-  const bool inl = active && abs(cu - u_pix - fu) <= 16 && abs(cv - v_pix - fv) <= 16;
+  // 2) bbox of the inlier centres (within 16 px of pixel + tile flow)
+  const bool inl = active && abs(cu - t.u_pix - fu) <= 16 && abs(cv - t.v_pix - fv) <= 16;
   int mnu = inl ? cu : INT_MAX, mxu = inl ? cu : INT_MIN;
   int mnv = inl ? cv : INT_MAX, mxv = inl ? cv : INT_MIN;
 #pragma unroll
@@ -151,7 +142,7 @@ __device__ __forceinline__ void refine_level(const h1* __restrict__ img, int H, 
   mxu = max(max(s_red[0][1], s_red[1][1]), max(s_red[2][1], s_red[3][1]));
   mnv = min(min(s_red[0][2], s_red[1][2]), min(s_red[2][2], s_red[3][2]));
   mxv = max(max(s_red[0][3], s_red[1][3]), max(s_red[2][3], s_red[3][3]));
-  if (mnu > mxu) {  // no inlier: any window (every active lane goes global)
+  if (mnu > mxu) {  // no inlier: any window (every active lane is an outlier)
     mnu = mxu = 0;
     mnv = mxv = 0;
   }
@@ -164,61 +155,68 @@ __device__ __forceinline__ void refine_level(const h1* __restrict__ img, int H, 
   const int u_lo = cu - RD, v_lo = cv - RD;
   const int bx = u_lo - wx0, by = v_lo - wy0;  // window coordinates of candidate (0, 0)
   const bool lane_in = active && bx >= 0 && bx + 2 * RD < RT_COLS && by >= 0 && by + 2 * RD < nrows;
-#ifdef M3S_REFINE_STATS  // (experiment builds only) per-level outlier lanes / waves
-  {
-    const uint64_t bm = __ballot(active && !lane_in);
-    if (lane == 0 && bm) {
-      atomicAdd(&g_refine_stats[2 * D], (unsigned long long)__popcll(bm));
-      atomicAdd(&g_refine_stats[2 * D + 1], 1ull);
-    }
+  const bool outl = active && !lane_in;
+  const uint64_t om = __ballot(outl);
+#ifdef M3S_REFINE_STATS
+  if (lane == 0 && om) {
+    atomicAdd(&g_refine_stats[2 * D], (unsigned long long)__popcll(om));
+    atomicAdd(&g_refine_stats[2 * D + 1], 1ull);
   }
 #endif
-#ifndef M3S_NO_COOP  // (timing experiment only: skips the outlier lanes)
-  if (__ballot(active && !lane_in)) refine_level_coop<D>(img, H, W, q, cu, cv, max_score, active && !lane_in, lane);
-#endif
+  if (om) {
+    if (t.olist != nullptr) {
+      // defer: one atomic per wave reserves the slots, lanes write {pixel, centre, max bits, level}
+      const int leader = __ffsll((long long)om) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(t.ocount, __popcll(om));
+      base = __shfl(base, leader, 64);
+      if (outl) {
+        const int rank = __popcll(om & ((1ull << lane) - 1ull));
+        const unsigned short mb = *reinterpret_cast<const unsigned short*>(&max_score);
+        t.olist[base + rank] = make_int4(t.bn, (cu & 0xffff) | (cv << 16), (int)mb | (D << 16), 0);
+        active = false;
+      }
+    } else {
+      // in place: the wave takes its outliers one at a time
+      uint64_t m = om;
+      while (m) {
+        const int src = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        int scu = __shfl(cu, src, 64), scv = __shfl(cv, src, 64);
+        const unsigned short mb0 = (unsigned short)__shfl((int)*reinterpret_cast<const unsigned short*>(&max_score),
+                                                          src, 64);
+        h1 smax = *reinterpret_cast<const h1*>(&mb0);
+        h2 sq[F / 2];
+#pragma unroll
+        for (int k = 0; k < F / 2; k++) {
+          const int v = __shfl(*reinterpret_cast<const int*>(&q[k]), src, 64);
+          sq[k] = *reinterpret_cast<const h2*>(&v);
+        }
+        wave_level<D>(t.img, H, W, sq, scu, scv, smax, lane);
+        if (lane == src) {
+          cu = scu;
+          cv = scv;
+          max_score = smax;
+        }
+      }
+    }
+  }
   h1 s[G * G];
 #pragma unroll
   for (int c = 0; c < G * G; c++) s[c] = (h1)0.0f;
-#if RT_NBUF == 2
-#pragma unroll
-  for (int chunk = 0; chunk < F / 8; chunk++) {
-    if (chunk == 0) {  // the first chunk of a level cannot be prefetched: its window needs the bbox
-      for (int y = wid; y < nrows; y += 4) {
-        const int gy = min(max(wy0 + y, 0), H - 1);
-        __builtin_amdgcn_global_load_lds((gvoid_t)(img + ((size_t)gy * W + gx) * F), (lvoid_t)&lds[0][y * RT_COLS],
-                                         16, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    if (chunk + 1 < F / 8) {  // one global_load_lds (64 lanes x 16 B) per window row, next chunk
-      for (int y = wid; y < nrows; y += 4) {
-        const int gy = min(max(wy0 + y, 0), H - 1);
-        __builtin_amdgcn_global_load_lds((gvoid_t)(img + ((size_t)gy * W + gx) * F + (chunk + 1) * 8),
-                                         (lvoid_t)&lds[(chunk + 1) & 1][y * RT_COLS], 16, 0, 0);
-      }
-    }
-    if (lane_in) score_chunk<D>(&lds[chunk & 1][by * RT_COLS + bx], &q[chunk * 4], s);
-    if (chunk + 1 < F / 8) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-#else
   __syncthreads();  // the reduction scratch aliases the window: its readers are done
 #pragma unroll
   for (int chunk = 0; chunk < F / 8; chunk++) {
     if (chunk) __syncthreads();  // previous chunk's readers are done
-    for (int y = wid; y < nrows; y += 4) {
+    for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
-      __builtin_amdgcn_global_load_lds((gvoid_t)(img + ((size_t)gy * W + gx) * F + chunk * 8),
-                                       (lvoid_t)&lds[0][y * RT_COLS], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gvoid_t)(t.img + ((size_t)gy * W + gx) * F + chunk * 8),
+                                       (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (lane_in) score_chunk<D>(&lds[0][by * RT_COLS + bx], &q[chunk * 4], s);
+    if (lane_in) score_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], s);
   }
-#endif
   if (lane_in) {  // scan-order arg-max: u outer, v inner, strict '>' (matching_kernels.cu:54-71)
     int bu = cu, bvv = cv;
 #pragma unroll
@@ -239,81 +237,148 @@ __device__ __forceinline__ void refine_level(const h1* __restrict__ img, int H, 
   }
 }
 
+template <bool P1_I64>
+__device__ __forceinline__ void load_p1(const void* p1v, size_t bn, int& cu, int& cv) {
+  if constexpr (P1_I64) {
+    cu = (int)reinterpret_cast<const int64_t*>(p1v)[bn * 2];
+    cv = (int)reinterpret_cast<const int64_t*>(p1v)[bn * 2 + 1];
+  } else {
+    cu = reinterpret_cast<const int*>(p1v)[bn * 2];
+    cv = reinterpret_cast<const int*>(p1v)[bn * 2 + 1];
+  }
+}
+
+template <bool LIN_OUT>
+__device__ __forceinline__ void store_out(void* outv, size_t bn, int W, int cu, int cv) {
+  if constexpr (LIN_OUT) {
+    reinterpret_cast<int64_t*>(outv)[bn] = (int64_t)cu + (int64_t)W * cv;
+  } else {
+    reinterpret_cast<int64_t*>(outv)[bn * 2] = cu;
+    reinterpret_cast<int64_t*>(outv)[bn * 2 + 1] = cv;
+  }
+}
+
 // P1_I64: p1 given as (B,N,2) int64 (reference op) else int32 (fused); LIN_OUT: write idx = u + W v.
 template <bool D21_F32, bool P1_I64, bool LIN_OUT>
-__global__ void __launch_bounds__(256, 2 * (3 - RT_NBUF)) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
+__global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
                                                              const void* __restrict__ p1v, void* __restrict__ outv,
                                                              int H, int W, int dilation_max, int tiles_x,
-                                                             int tiles_per_img, int nblocks) {
+                                                             int tiles_per_img, int nblocks, int4* olist,
+                                                             int* ocount) {
   constexpr int F = 24;
-  __shared__ uint4 lds[RT_NBUF][RT_ROWS * RT_COLS];
-  // level-start reductions run while buffer 1 is idle (its last readers passed a barrier, its next
-  // fill is issued after the chunk-0 barrier)
-  int(*s_red)[4] = reinterpret_cast<int(*)[4]>(&lds[RT_NBUF - 1][0]);
+  __shared__ uint4 lds[RT_ROWS * RT_COLS];
+  int(*s_red)[4] = reinterpret_cast<int(*)[4]>(&lds[0]);  // level-start reductions alias the window
   const int lb = xcd_remap(blockIdx.x, nblocks);
-  const int b = lb / tiles_per_img, t = lb % tiles_per_img;
-  const int tx = t % tiles_x, ty = t / tiles_x;
-  const int lx = threadIdx.x % RT_TW, ly = threadIdx.x / RT_TW;
-  const int u_pix = tx * RT_TW + lx, v_pix = ty * RT_TH + ly;
-  const bool active = u_pix < W && v_pix < H;
+  const int b = lb / tiles_per_img, tt = lb % tiles_per_img;
+  const int tx = tt % tiles_x, ty = tt / tiles_x;
+  TileCtx t;
+  t.H = H;
+  t.W = W;
+  t.lane = threadIdx.x & 63;
+  t.wid = threadIdx.x >> 6;
+  t.u_pix = tx * RT_TW + threadIdx.x % RT_TW;
+  t.v_pix = ty * RT_TH + threadIdx.x / RT_TW;
+  t.olist = olist;
+  t.ocount = ocount;
+  bool active = t.u_pix < W && t.v_pix < H;
   const int N = H * W;
-  const size_t bn = (size_t)b * N + (size_t)v_pix * W + u_pix;
-  const h1* img = D11h + (size_t)b * N * F;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const size_t bn = (size_t)b * N + (size_t)t.v_pix * W + t.u_pix;
+  t.bn = (int)bn;
+  t.img = D11h + (size_t)b * N * F;
   h2 q[F / 2];
   int cu = 0, cv = 0;
   if (active) {
     load_query<F, D21_F32>(D21, bn, q);
-    if constexpr (P1_I64) {
-      cu = (int)reinterpret_cast<const int64_t*>(p1v)[bn * 2];
-      cv = (int)reinterpret_cast<const int64_t*>(p1v)[bn * 2 + 1];
-    } else {
-      cu = reinterpret_cast<const int*>(p1v)[bn * 2];
-      cv = reinterpret_cast<const int*>(p1v)[bn * 2 + 1];
-    }
+    load_p1<P1_I64>(p1v, bn, cu, cv);
   } else {
 #pragma unroll
     for (int k = 0; k < F / 2; k++) q[k] = h2{(h1)0.0f, (h1)0.0f};
   }
-  h1 max_score = (h1)0.0f;  // numeric_limits<c10::Half>::min() == +0, never reset between levels
+  const bool mine = active;  // deferred pixels are written by refine_outlier_kernel
+  h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
   for (int d = dilation_max; d > 0; d--) {
     switch (d) {
-      case 8: refine_level<8>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 7: refine_level<7>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 6: refine_level<6>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 5: refine_level<5>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 4: refine_level<4>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 3: refine_level<3>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      case 2: refine_level<2>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
-      default: refine_level<1>(img, H, W, active, q, cu, cv, max_score, lds, s_red, lane, wid, u_pix, v_pix); break;
+      case 8: refine_level<8>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 7: refine_level<7>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 6: refine_level<6>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 5: refine_level<5>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 4: refine_level<4>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 3: refine_level<3>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 2: refine_level<2>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      default: refine_level<1>(t, active, q, cu, cv, max_score, lds, s_red); break;
     }
   }
-  if (active) {
-    if constexpr (LIN_OUT) {
-      reinterpret_cast<int64_t*>(outv)[bn] = (int64_t)cu + (int64_t)W * cv;
-    } else {
-      reinterpret_cast<int64_t*>(outv)[bn * 2] = cu;
-      reinterpret_cast<int64_t*>(outv)[bn * 2 + 1] = cv;
+  if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
+}
+
+// Finishes the deferred pixels: one wave per pixel, levels d0..1 by wave_level (grid-stride over
+// the list; the count is read on the device, so the launch needs no host sync).
+template <bool D21_F32, bool LIN_OUT>
+__global__ void __launch_bounds__(256) refine_outlier_kernel(const h1* __restrict__ D11h,
+                                                             const void* __restrict__ D21, void* __restrict__ outv,
+                                                             int H, int W, const int4* __restrict__ olist,
+                                                             const int* __restrict__ ocount) {
+  constexpr int F = 24;
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  const int count = *ocount;
+  const int N = H * W;
+  for (int o = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); o < count; o += nwaves) {
+    const int4 r = olist[o];
+    const size_t bn = (size_t)r.x;
+    int cu = (int)(short)(r.y & 0xffff), cv = r.y >> 16;
+    const unsigned short mb = (unsigned short)(r.z & 0xffff);
+    h1 max_score = *reinterpret_cast<const h1*>(&mb);
+    const int d0 = r.z >> 16;
+    const h1* img = D11h + (bn / N) * (size_t)N * F;
+    h2 q[F / 2];
+    load_query<F, D21_F32>(D21, bn, q);
+    for (int d = d0; d > 0; d--) {
+      switch (d) {
+        case 8: wave_level<8>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 7: wave_level<7>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 6: wave_level<6>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 5: wave_level<5>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 4: wave_level<4>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 3: wave_level<3>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 2: wave_level<2>(img, H, W, q, cu, cv, max_score, lane); break;
+        default: wave_level<1>(img, H, W, q, cu, cv, max_score, lane); break;
+      }
     }
+    if (lane == 0) store_out<LIN_OUT>(outv, bn, W, cu, cv);
   }
 }
 
 }  // namespace m3s
 
 // D21 f32 + p1 int32 -> idx (fused path) or D21 f16 + p1 int64 -> p1_new (reference op).
-// Returns hipErrorNotSupported when the shape is not eligible (caller falls back to per-pixel).
+// olist/ocount (nullable): deferred-outlier list of >= B*H*W int4 and its counter, zeroed on the
+// stream before this launch. Returns hipErrorNotSupported when the shape is not eligible (the
+// caller falls back to the per-pixel kernels).
 extern "C" hipError_t m3s_launch_refine_tile(const void* D11h, const void* D21, const void* p1, void* out, int B,
                                              int H, int W, int F, int radius, int dilation_max, int fused,
-                                             hipStream_t s) {
+                                             void* olist, int* ocount, hipStream_t s) {
   if (F != 24 || radius != 3 || dilation_max < 1 || dilation_max > 8) return hipErrorNotSupported;
+  if ((long long)B * H * W >= (1ll << 31) || H >= 32768 || W >= 32768) return hipErrorNotSupported;
   const int tx = (W + RT_TW - 1) / RT_TW, ty = (H + RT_TH - 1) / RT_TH, nb = tx * ty * B;
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
+  int4* ol = reinterpret_cast<int4*>(olist);
+  if (ol == nullptr) ocount = nullptr;
   if (fused)
     hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true>), dim3(nb), dim3(256), 0, s, a, D21, p1, out, H, W,
-                       dilation_max, tx, tx * ty, nb);
+                       dilation_max, tx, tx * ty, nb, ol, ocount);
   else
     hipLaunchKernelGGL((m3s::refine_tile_kernel<false, true, false>), dim3(nb), dim3(256), 0, s, a, D21, p1, out, H,
-                       W, dilation_max, tx, tx * ty, nb);
+                       W, dilation_max, tx, tx * ty, nb, ol, ocount);
+  if (ol != nullptr) {
+    const int ob = 1024;  // 4096 waves: one pass over a few thousand deferred pixels, idle waves exit
+    if (fused)
+      hipLaunchKernelGGL((m3s::refine_outlier_kernel<true, true>), dim3(ob), dim3(256), 0, s, a, D21, out, H, W, ol,
+                         ocount);
+    else
+      hipLaunchKernelGGL((m3s::refine_outlier_kernel<false, false>), dim3(ob), dim3(256), 0, s, a, D21, out, H, W,
+                         ol, ocount);
+  }
   return hipGetLastError();
 }
 
