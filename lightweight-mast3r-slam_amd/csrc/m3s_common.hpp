@@ -166,4 +166,11 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Bijective block remap (cdna guide §5 "XCD swizzle"): hardware deals block b to XCD b % 8; this
+// returns the logical block so that each XCD gets one contiguous run of logical blocks.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 }  // namespace m3s

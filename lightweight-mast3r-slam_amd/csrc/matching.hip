@@ -87,10 +87,15 @@ __device__ __forceinline__ void bilin_w(float u, float v, int& u11, int& v11, fl
   v11 = (int)floorf(v);
   const float du = u - (float)u11;
   const float dv = v - (float)v11;
+  // (1.0-du)*dv etc. are evaluated in double by the reference (:161-164). u, v >= 1 after clamping,
+  // so du, dv are multiples of ulp(u) >= 2^-23 and 1-du, 1-dv are exact in float; the double
+  // product of two exact floats is then rounded once to float — the same value as this float
+  // product (no fp64 needed, bit-identical).
+  const float cu = 1.0f - du, cv = 1.0f - dv;
   w[0] = du * dv;
-  w[1] = (float)((1.0 - (double)du) * (double)dv);  // (1.0-du)*dv in double (:162)
-  w[2] = (float)((double)du * (1.0 - (double)dv));
-  w[3] = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+  w[1] = cu * dv;
+  w[2] = du * cv;
+  w[3] = cu * cv;
 }
 
 template <int NC>
@@ -110,11 +115,15 @@ __device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, i
   u = fminf(fmaxf(u, 1.0f), (float)(W - 2));
   v = fminf(fmaxf(v, 1.0f), (float)(H - 2));
   float lambda = lambda_init;
+  // The reference samples (u, v) at the top of every iteration and (u_new, v_new) for the new cost.
+  // The top-of-loop sample always equals the previous iteration's accepted sample (u_new) or its own
+  // previous value (rejected), so the 9-channel sample is carried instead of refetched: one
+  // dependent gather per iteration instead of two, identical values.
+  int u11, v11;
+  float w[4], s[9];
+  bilin_w(u, v, u11, v11, w);
+  bilin_sample<9>(img, W, u11, v11, w, s);
   for (int i = 0; i < max_iter; i++) {
-    int u11, v11;
-    float w[4], s[9];
-    bilin_w(u, v, u11, v11, w);
-    bilin_sample<9>(img, W, u11, v11, w, s);
     // 1.0/r_norm in double then float == IEEE float division (53 >= 2*24+2, innocuous double rounding)
     float r_norm_inv = 1.0f / sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
     const float e0 = s[0] * r_norm_inv - p[0];
@@ -134,16 +143,18 @@ __device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, i
     u_new = fminf(fmaxf(u_new, 1.0f), (float)(W - 2));
     v_new = fminf(fmaxf(v_new, 1.0f), (float)(H - 2));
     bilin_w(u_new, v_new, u11, v11, w);
-    float r[3];
-    bilin_sample<3>(img, W, u11, v11, w, r);
-    r_norm_inv = 1.0f / sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    const float f0 = r[0] * r_norm_inv - p[0];
-    const float f1 = r[1] * r_norm_inv - p[1];
-    const float f2 = r[2] * r_norm_inv - p[2];
+    float t[9];
+    bilin_sample<9>(img, W, u11, v11, w, t);
+    r_norm_inv = 1.0f / sqrtf(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+    const float f0 = t[0] * r_norm_inv - p[0];
+    const float f1 = t[1] * r_norm_inv - p[1];
+    const float f2 = t[2] * r_norm_inv - p[2];
     const float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
     if (new_cost < cost) {
       u = u_new;
       v = v_new;
+#pragma unroll
+      for (int k = 0; k < 9; k++) s[k] = t[k];
       lambda = (float)((double)lambda * 0.1);
       conv = new_cost < cost_thresh;
     } else {
@@ -179,7 +190,8 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
     const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
     int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter) {
   const int N = H * W;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  // contiguous pixel runs per XCD: each XCD's L2 then holds the rays rows its LM gathers touch
+  const int n = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (zero_counter != nullptr && n == 0 && b == 0) *zero_counter = 0;  // refine's outlier list (next launch)
   if (n >= N) return;

@@ -37,11 +37,6 @@ namespace m3s {
 typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
 
-__device__ __forceinline__ int xcd_remap(int b, int nb) {  // bijective (cdna guide §5 "XCD swizzle")
-  const int q = nb / 8, r = nb % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
 #ifdef M3S_REFINE_STATS  // (experiment builds only) per-level deferred lanes / waves
 __device__ unsigned long long g_refine_stats[32];
 #endif
