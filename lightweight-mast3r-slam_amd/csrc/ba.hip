@@ -269,75 +269,118 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 // ------------------------------------------------------------------------------------------
 // dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) chol_diag_kernel(double* __restrict__ H, int n, int k0, int* __restrict__ info,
-                                                        const int* __restrict__ done) {
-  if (*done) return;
-  const int kb = min(CH_NB, n - k0);
-  __shared__ double T[CH_NB][CH_NB + 1];
-  for (int t = threadIdx.x; t < kb * kb; t += blockDim.x) {
-    const int i = t / kb, j = t % kb;
-    T[i][j] = (j <= i) ? H[(size_t)(k0 + i) * n + k0 + j] : 0.0;
-  }
-  __syncthreads();
-  for (int j = 0; j < kb; j++) {
-    if (threadIdx.x == 0) {
-      double d = T[j][j];
-      if (!(d > 0.0)) {
-        *info = 1;
-        d = 1.0;
-      }
-      T[j][j] = sqrt(d);
-    }
-    __syncthreads();
-    const double djj = T[j][j];
-    for (int i = j + 1 + threadIdx.x; i < kb; i += blockDim.x) T[i][j] /= djj;
-    __syncthreads();
-    const int m = kb - j - 1;  // trailing (m x m) lower update
-    for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
-      const int i = j + 1 + t / m, c = j + 1 + t % m;
-      if (c <= i) T[i][c] -= T[i][j] * T[c][j];
-    }
-    __syncthreads();
-  }
-  for (int t = threadIdx.x; t < kb * kb; t += blockDim.x) {
-    const int i = t / kb, j = t % kb;
-    if (j <= i) H[(size_t)(k0 + i) * n + k0 + j] = T[i][j];
+// lanes of one wave exchanging data through LDS: a compiler memory barrier (the hardware returns a
+// wave's LDS accesses in order)
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double bcast_lane(double v, int src) {
+  int2 x = *reinterpret_cast<int2*>(&v);
+  x.x = __builtin_amdgcn_readlane(x.x, src);
+  x.y = __builtin_amdgcn_readlane(x.y, src);
+  return *reinterpret_cast<double*>(&x);
+}
+
+// Stage a 64-row block of H (rows r0.., columns k0..k0+63) into LDS with coalesced loads (lane =
+// column), all loads of a 32-row batch in flight before the stores.
+__device__ __forceinline__ void stage_rows(const double* __restrict__ H, int n, int r0, int nr, int k0, int kb,
+                                           double (*S)[CH_NB + 1], int lane) {
+  const int lc = min(lane, kb - 1);
+  for (int t0 = 0; t0 < CH_NB; t0 += 32) {
+    double v[32];
+#pragma unroll
+    for (int u = 0; u < 32; u++) v[u] = H[(size_t)(r0 + min(t0 + u, nr - 1)) * n + k0 + lc];
+#pragma unroll
+    for (int u = 0; u < 32; u++) S[t0 + u][lane] = (t0 + u < nr && lane < kb) ? v[u] : 0.0;
   }
 }
 
-// rows r in [k0+kb, n] (row n = rhs): L21 = A21 L11^-T, 64 rows per block, right-looking over
-// the panel's columns so all 256 lanes work between the 2*kb barriers
-__global__ void __launch_bounds__(256) chol_trsm_kernel(double* __restrict__ H, int n, int k0,
-                                                        const int* __restrict__ done) {
+// Right-looking column step J of the register-row diagonal factorisation: pivot and column
+// multipliers broadcast with readlane (no LDS round trip), rank-1 update of the lane's own row.
+// Rows/columns >= kb are padded with the identity, so every step is valid and the padding inert.
+template <int J>
+__device__ __forceinline__ void diag_step(double (&r)[CH_NB], int lane, bool& bad) {
+  if constexpr (J < CH_NB) {
+    double d = bcast_lane(r[J], J);
+    if (!(d > 0.0)) {
+      bad = true;
+      d = 1.0;
+    }
+    const double sj = sqrt(d);
+    const double inv = 1.0 / sj;
+    // unconditional multiplier (a lane-dependent select here makes the allocator spill r[]); lanes
+    // <= J only disturb their own strictly-upper entries, which are never read
+    const double l = r[J] * inv;
+    r[J] = lane == J ? sj : (lane > J ? l : r[J]);
+#pragma unroll
+    for (int c = J + 1; c < CH_NB; c++) r[c] -= l * bcast_lane(l, c);
+    diag_step<J + 1>(r, lane, bad);
+  }
+}
+
+// 64x64 diagonal block by one wave: lane i keeps row i in registers (static indices: the steps are
+// compile-time), ~2k FMAs + 4k readlanes per lane, no barriers. Also writes L11^T to Lt for the
+// panel solve (scalar-loadable there).
+__global__ void __launch_bounds__(64) chol_diag_kernel(double* __restrict__ H, double* __restrict__ Lt, int n, int k0,
+                                                       int* __restrict__ info, const int* __restrict__ done) {
   if (*done) return;
   const int kb = min(CH_NB, n - k0);
-  __shared__ double Ls[CH_NB][CH_NB + 1];
-  __shared__ double X[CH_NB][CH_NB + 1];
-  for (int t = threadIdx.x; t < kb * kb; t += blockDim.x) {
-    const int i = t / kb, j = t % kb;
-    Ls[i][j] = (j <= i) ? H[(size_t)(k0 + i) * n + k0 + j] : 0.0;
+  __shared__ double S[CH_NB][CH_NB + 1];
+  const int lane = threadIdx.x;
+  stage_rows(H, n, k0, kb, k0, kb, S, lane);
+  wave_sync();
+  double r[CH_NB];
+#pragma unroll
+  for (int c = 0; c < CH_NB; c++) r[c] = (lane < kb && c < kb) ? S[lane][c] : (c == lane ? 1.0 : 0.0);
+  bool bad = false;
+  diag_step<0>(r, lane, bad);
+  if (bad && lane == 0) *info = 1;
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < CH_NB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
+  wave_sync();
+  for (int t = 0; t < kb; t++)  // coalesced write-back of the lower triangle (lane = column)
+    if (lane <= t) H[(size_t)(k0 + t) * n + k0 + lane] = S[t][lane];
+  for (int t = 0; t < CH_NB; t++) Lt[t * CH_NB + lane] = S[lane][t];  // Lt[j][k] = L[k][j] (padded)
+}
+
+// Right-looking step J of the register-row forward substitution: x_J /= L_JJ, then fold x_J into
+// the later columns with column J of L11 — uniform addresses of a restrict-const buffer, so the
+// compiler reads them with scalar loads (SGPR operands, no LDS).
+template <int J>
+__device__ __forceinline__ void trsm_step(double (&x)[CH_NB], const double* __restrict__ Lt) {
+  if constexpr (J < CH_NB) {
+    x[J] /= Lt[J * CH_NB + J];
+#pragma unroll
+    for (int k = J + 1; k < CH_NB; k++) x[k] -= x[J] * Lt[J * CH_NB + k];
+    trsm_step<J + 1>(x, Lt);
   }
+}
+
+// rows r in [k0+kb, n] (row n = rhs): L21 = A21 L11^-T. One wave per 64 rows, lane = row in
+// registers; L11^T from the diagonal kernel (padding: identity).
+__global__ void __launch_bounds__(64) chol_trsm_kernel(double* __restrict__ H, const double* __restrict__ Lt, int n,
+                                                       int k0, const int* __restrict__ done) {
+  if (*done) return;
+  const int kb = min(CH_NB, n - k0);
+  __shared__ double X[CH_NB][CH_NB + 1];
+  const int lane = threadIdx.x;
   const int r0 = k0 + kb + blockIdx.x * CH_NB;
   const int nr = min(CH_NB, n + 1 - r0);
-  for (int t = threadIdx.x; t < nr * kb; t += blockDim.x) {
-    const int i = t / kb, j = t % kb;
-    X[i][j] = H[(size_t)(r0 + i) * n + k0 + j];
-  }
-  __syncthreads();
-  for (int j = 0; j < kb; j++) {
-    if (threadIdx.x < nr) X[threadIdx.x][j] /= Ls[j][j];
-    __syncthreads();
-    const int m = kb - j - 1;
-    for (int t = threadIdx.x; t < nr * m; t += blockDim.x) {
-      const int i = t / m, c = j + 1 + t % m;
-      X[i][c] -= X[i][j] * Ls[c][j];
-    }
-    __syncthreads();
-  }
-  for (int t = threadIdx.x; t < nr * kb; t += blockDim.x) {
-    const int ii = t / kb, j = t % kb;
-    H[(size_t)(r0 + ii) * n + k0 + j] = X[ii][j];
-  }
+  stage_rows(H, n, r0, nr, k0, kb, X, lane);
+  wave_sync();
+  double x[CH_NB];
+#pragma unroll
+  for (int c = 0; c < CH_NB; c++) x[c] = X[lane][c];
+  trsm_step<0>(x, Lt);
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < CH_NB; c++) X[lane][c] = x[c];
+  wave_sync();
+  for (int t = 0; t < nr; t++)
+    if (lane < kb) H[(size_t)(r0 + t) * n + k0 + lane] = X[t][lane];
 }
 
 // trailing update A22 -= L21 L21^T over 64x64 lower tiles; rows [s, n], cols [s, n-1], s = k0+kb
@@ -353,10 +396,21 @@ __global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H
   const int nr = min(CH_NB, n + 1 - r0), nc = min(CH_NB, n - c0);
   __shared__ double A[CH_NB][CH_NB + 1];
   __shared__ double B[CH_NB][CH_NB + 1];
-  for (int t = threadIdx.x; t < CH_NB * kb; t += blockDim.x) {
-    const int i = t / kb, k = t % kb;
-    A[i][k] = i < nr ? H[(size_t)(r0 + i) * n + k0 + k] : 0.0;
-    B[i][k] = i < nc ? H[(size_t)(c0 + i) * n + k0 + k] : 0.0;
+  {  // 16 + 16 per lane, branch-free, all loads issued before the LDS stores
+    double av[16], bv[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / CH_NB, k = t % CH_NB;
+      const int kc = min(k, kb - 1);
+      av[u] = H[(size_t)(r0 + min(i, nr - 1)) * n + k0 + kc];
+      bv[u] = H[(size_t)(c0 + min(i, nc - 1)) * n + k0 + kc];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / CH_NB, k = t % CH_NB;
+      A[i][k] = (i < nr && k < kb) ? av[u] : 0.0;
+      B[i][k] = (i < nc && k < kb) ? bv[u] : 0.0;
+    }
   }
   __syncthreads();
   const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;  // 4x4 outputs per lane
@@ -400,13 +454,28 @@ __global__ void __launch_bounds__(256) chol_back_kernel(const double* __restrict
   __shared__ double part[4][CH_NB];
   __shared__ double Ld[CH_NB][CH_NB + 1];
   const int c = threadIdx.x % CH_NB, g = threadIdx.x / CH_NB;
-  double s = 0.0;
-  if (c < kb)
-    for (int r = k0 + kb + g; r < n; r += 4) s += H[(size_t)r * n + k0 + c] * x[r];
-  part[g][c] = s;
-  for (int t = threadIdx.x; t < kb * kb; t += blockDim.x) {
-    const int i = t / kb, j = t % kb;
-    Ld[i][j] = (j <= i) ? H[(size_t)(k0 + i) * n + k0 + j] : 0.0;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // independent partial sums: 4 row loads in flight per lane
+  if (c < kb) {
+    int r = k0 + kb + g;
+    for (; r + 12 < n; r += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc[u] += H[(size_t)(r + 4 * u) * n + k0 + c] * x[r + 4 * u];
+    }
+    for (; r < n; r += 4) acc[0] += H[(size_t)r * n + k0 + c] * x[r];
+  }
+  part[g][c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  {
+    double lv[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / CH_NB, j = t % CH_NB;
+      lv[u] = H[(size_t)(k0 + min(i, kb - 1)) * n + k0 + min(j, kb - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / CH_NB, j = t % CH_NB;
+      Ld[i][j] = (i < kb && j <= i) ? lv[u] : 0.0;
+    }
   }
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -470,11 +539,11 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
     hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows), dim3(64), 0, s, *a, n, nblocks);
     for (int k0 = 0; k0 < n; k0 += CH_NB) {
       const int kb = n - k0 < CH_NB ? n - k0 : CH_NB;
-      hipLaunchKernelGGL(m3s::chol_diag_kernel, dim3(1), dim3(256), 0, s, a->H, n, k0, a->info, a->done);
+      hipLaunchKernelGGL(m3s::chol_diag_kernel, dim3(1), dim3(64), 0, s, a->H, a->Lt, n, k0, a->info, a->done);
       const int rows = n + 1 - (k0 + kb);
       if (rows > 0) {
         const int tr = (rows + CH_NB - 1) / CH_NB;
-        hipLaunchKernelGGL(m3s::chol_trsm_kernel, dim3(tr), dim3(256), 0, s, a->H, n, k0, a->done);
+        hipLaunchKernelGGL(m3s::chol_trsm_kernel, dim3(tr), dim3(64), 0, s, a->H, a->Lt, n, k0, a->done);
         const int tc = (n - (k0 + kb) + CH_NB - 1) / CH_NB;
         if (tc > 0) hipLaunchKernelGGL(m3s::chol_update_kernel, dim3(tr, tc), dim3(256), 0, s, a->H, n, k0, a->done);
       }
