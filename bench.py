@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--mode", choices=["calib", "rays"], default="calib")
     ap.add_argument("--ring", type=int, default=6, help="distinct synthetic pairs cycled (ring > L3)")
-    ap.add_argument("--ba-kf", type=int, default=64)
+    ap.add_argument("--ba-kf", type=int, default=256)  # C5: 256-keyframe synthetic factor graph
     ap.add_argument("--ba-h", type=int, default=384)
     ap.add_argument("--ba-w", type=int, default=512)
     ap.add_argument("--ba-iters", type=int, default=10)

@@ -11,7 +11,8 @@
 //   * ba_lin: (edge, point-chunk) blocks. Because Ji = -Jj and Jj = A_i J_local with a per-edge
 //     7x7 adjoint map A_i (gn_kernels.cu:277-297 is linear in the row), each lane accumulates only
 //     the 28-entry local normal matrix L = sum w J J^T and the 7-entry v = sum w e J in registers
-//     (instead of 105 + 14 transformed entries) and the per-edge transform is applied once.
+//     (instead of 105 + 14 transformed entries, products/sums in fp64, structural zeros skipped)
+//     and the per-edge transform is applied once.
 //   * ba_edge: per-edge fp64 reduction of the chunk partials and M = A L A^T, g = A v.
 //     The (E,36) edge-sum rows are the only data a multi-GPU run all-reduces.
 //   * ba_assemble: deterministic block-sparse scatter (host-built CSR of contributions per 7x7
@@ -31,18 +32,33 @@ namespace m3s {
 // ------------------------------------------------------------------------------------------
 // linearisation
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void acc_local(float* L, float* v, const float J[7], float w, float e) {
+// MASK: the row's structurally nonzero Jacobian entries (bit c). Products with a structural zero
+// are skipped: for finite weights they add an exact +-0 to the sum, so the result is unchanged
+// (the reference computes them; ~45% of the FMAs in rays mode).
+// Products and sums in fp64 from the fp32 rows: fp64 FMA issues at the fp32 (unpacked) rate on
+// CDNA, and it keeps the whole BA within 1e-5 of the fp64 truth (fp32 products put the
+// ill-conditioned 6-KF golden at ~1.2e-5).
+template <unsigned MASK>
+__device__ __forceinline__ void acc_local(double* L, double* v, const float J[7], float w, float e) {
+  double Jd[7];
+#pragma unroll
+  for (int c = 0; c < 7; c++) Jd[c] = (double)J[c];
+  const double wd = (double)w, ed = (double)e;
   int l = 0;
 #pragma unroll
   for (int c = 0; c < 7; c++) {
-    const float wj = w * J[c];
+    const double wj = wd * Jd[c];
 #pragma unroll
-    for (int d = c; d < 7; d++) L[l++] += wj * J[d];
-    v[c] += wj * e;
+    for (int d = c; d < 7; d++) {
+      if ((MASK >> c) & (MASK >> d) & 1u) L[l] += wj * Jd[d];
+      l++;
+    }
+    if ((MASK >> c) & 1u) v[c] += wj * ed;
   }
 }
 
-__global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
+template <int MODE>  // specialised per residual type: one mode's registers, not the union of three
+__global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
   if (*a.done) return;
   const int e = blockIdx.x / p.chunks;
   const int chunk = blockIdx.x % p.chunks;
@@ -55,11 +71,11 @@ __global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
     Tj[c] = a.Twc[jx * 8 + c];
   }
   relSim3(Ti, Tj, Tij);
-  float L[28], v[7];
+  double L[28], v[7];
 #pragma unroll
-  for (int c = 0; c < 28; c++) L[c] = 0.0f;
+  for (int c = 0; c < 28; c++) L[c] = 0.0;
 #pragma unroll
-  for (int c = 0; c < 7; c++) v[c] = 0.0f;
+  for (int c = 0; c < 7; c++) v[c] = 0.0;
   const size_t eoff = (size_t)(e + p.edge_offset) * N;
   const float* Xi_base = a.Xs + (size_t)ix * N * 3;
   const float* Xj_base = a.Xs + (size_t)jx * N * 3;
@@ -86,17 +102,17 @@ __global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
     const float cj = Cj_base[k];
     bool valid = vm && (q > p.Q_thresh) && (ci > p.C_thresh) && (cj > p.C_thresh);
     const float sqq = sqrtf(q);
-    if (p.mode == BA_MODE_POINTS) {
+    if constexpr (MODE == BA_MODE_POINTS) {
       const float err[3] = {Y[0] - Xi[0], Y[1] - Xi[1], Y[2] - Xi[2]};
       const float sw = valid ? p.inv_a * sqq : 0.0f;
       const float wc = sw * sw;
       const float J0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
       const float J1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
       const float J2[7] = {0.0f, 0.0f, 1.0f, Y[1], -Y[0], 0.0f, Y[2]};
-      acc_local(L, v, J0, huber_ba(sw * err[0]) * wc, err[0]);
-      acc_local(L, v, J1, huber_ba(sw * err[1]) * wc, err[1]);
-      acc_local(L, v, J2, huber_ba(sw * err[2]) * wc, err[2]);
-    } else if (p.mode == BA_MODE_RAYS) {
+      acc_local<0b1110001>(L, v, J0, huber_ba(sw * err[0]) * wc, err[0]);  // {0,4,5,6}
+      acc_local<0b1101010>(L, v, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
+      acc_local<0b1011100>(L, v, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
+    } else if constexpr (MODE == BA_MODE_RAYS) {
       const float n1i = sqrtf(Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2]);
       const float n1i_inv = 1.0f / n1i;
       const float n2j = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
@@ -118,10 +134,10 @@ __global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
       const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.0f, rj[0], 0.0f};
       const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.0f, 0.0f};
       const float J3[7] = {rj[0], rj[1], rj[2], 0.0f, 0.0f, 0.0f, n1j};
-      acc_local(L, v, J0, huber_ba(swr * err[0]) * wr, err[0]);
-      acc_local(L, v, J1, huber_ba(swr * err[1]) * wr, err[1]);
-      acc_local(L, v, J2, huber_ba(swr * err[2]) * wr, err[2]);
-      acc_local(L, v, J3, huber_ba(swd * err[3]) * wd, err[3]);
+      acc_local<0b0110111>(L, v, J0, huber_ba(swr * err[0]) * wr, err[0]);  // {0,1,2,4,5}
+      acc_local<0b0101111>(L, v, J1, huber_ba(swr * err[1]) * wr, err[1]);  // {0,1,2,3,5}
+      acc_local<0b0011111>(L, v, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
+      acc_local<0b1000111>(L, v, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
       const int u_t = (int)(ind % p.W), v_t = (int)(ind / p.W);
       const bool valid_z = (Y[2] > p.z_eps) && (Xi[2] > p.z_eps);
@@ -141,9 +157,9 @@ __global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
       const float J0[7] = {fx * zj_inv, 0.0f, -fx * xz * zj_inv, -fx * xz * yz, fx * (1 + xz * xz), -fx * yz, 0.0f};
       const float J1[7] = {0.0f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1 + yz * yz), fy * xz * yz, fy * xz, 0.0f};
       const float J2[7] = {0.0f, 0.0f, zj_inv, yz, -xz, 0.0f, 1.0f};
-      acc_local(L, v, J0, huber_ba(swp * err[0]) * wp, err[0]);
-      acc_local(L, v, J1, huber_ba(swp * err[1]) * wp, err[1]);
-      acc_local(L, v, J2, huber_ba(swd * err[2]) * wd, err[2]);
+      acc_local<0b0111101>(L, v, J0, huber_ba(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
+      acc_local<0b0111110>(L, v, J1, huber_ba(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
+      acc_local<0b1011100>(L, v, J2, huber_ba(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
   }
   // wave64 butterfly in fp64, then 4 waves through LDS
@@ -151,12 +167,12 @@ __global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs a, BaParams p) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < 28; c++) {
-    const double t = wave_sum((double)L[c]);
+    const double t = wave_sum(L[c]);
     if (lane == 0) s_part[wid][c] = t;
   }
 #pragma unroll
   for (int c = 0; c < 7; c++) {
-    const double t = wave_sum((double)v[c]);
+    const double t = wave_sum(v[c]);
     if (lane == 0) s_part[wid][28 + c] = t;
   }
   __syncthreads();
@@ -526,7 +542,13 @@ __global__ void __launch_bounds__(256) ba_retr_kernel(BaArgs a, int K, int n, fl
 // ------------------------------------------------------------------------------------------
 extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
-  hipLaunchKernelGGL(m3s::ba_lin_kernel, dim3(E_local * p->chunks), dim3(256), 0, s, *a, *p);
+  const dim3 g(E_local * p->chunks);
+  if (p->mode == BA_MODE_POINTS)
+    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p);
+  else if (p->mode == BA_MODE_RAYS)
+    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p);
+  else
+    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p);
   hipLaunchKernelGGL(m3s::ba_edge_kernel, dim3(E_local), dim3(64), 0, s, *a, *p, E_local);
   return hipGetLastError();
 }

@@ -28,6 +28,28 @@ _u16p = ctypes.POINTER(ctypes.c_uint16)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 
 
+_LIB64 = None
+
+
+def lib64():
+    """The fp64 truth build of the same restatement (oracle/Makefile F64): BA only."""
+    global _LIB64
+    if _LIB64 is None:
+        path = os.path.join(_HERE, "liboracle_m3s_f64.so")
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.check_call(["make", "-C", _HERE, "-s", "liboracle_m3s_f64.so"])
+        L = ctypes.CDLL(path)
+        L.m3o_gauss_newton.argtypes = (
+            [ctypes.c_int, _f64p, _f64p, _f64p] + [ctypes.c_int] * 3 + [_i64p, _i64p, _i64p, _u8p, _f64p, _f64p]
+            + [ctypes.c_int, ctypes.c_double, _f64p]
+        )
+        L.m3o_gauss_newton.restype = ctypes.c_int
+        _LIB64 = L
+    return _LIB64
+
+
 def lib():
     """Load (building on demand) the oracle C library."""
     global _LIB
@@ -138,6 +160,26 @@ def gauss_newton(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, params, max_iter, del
                                  _p(dx, _f32p))
     if its < 0:
         raise RuntimeError("oracle gauss_newton: more unique keyframe ids than poses")
+    return Twc, dx, its
+
+
+def gauss_newton_f64(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, params, max_iter, delta_thresh):
+    """fp64 truth of gauss_newton (every float of the restatement computed in double)."""
+    Twc = np.array(Twc, np.float64, copy=True, order="C")
+    Xs, Cs = _c(Xs, np.float64), _c(Cs, np.float64)
+    K, N = Xs.shape[:2]
+    ii, jj = _c(ii, np.int64), _c(jj, np.int64)
+    E = ii.shape[0]
+    idx = _c(idx, np.int64).reshape(E, N)
+    valid = _c(valid, np.uint8).reshape(E, N)
+    Q = _c(Q, np.float64).reshape(E, N)
+    dx = np.zeros((max(K - 1, 0), 7), np.float64)
+    its = lib64().m3o_gauss_newton(_MODES[mode], _p(Twc, _f64p), _p(Xs, _f64p), _p(Cs, _f64p), K, N, E,
+                                   _p(ii, _i64p), _p(jj, _i64p), _p(idx, _i64p), _p(valid, _u8p), _p(Q, _f64p),
+                                   _p(_c(params, np.float64), _f64p), int(max_iter), float(delta_thresh),
+                                   _p(dx, _f64p))
+    if its < 0:
+        raise RuntimeError("oracle gauss_newton_f64: more unique keyframe ids than poses")
     return Twc, dx, its
 
 

@@ -90,7 +90,18 @@ def test_factor_graph_matches_reference(golden, mode):
     fg.Q_ii2jj, fg.Q_jj2ii = d(g["Q2"][:E]), d(g["Q2"][E:])
     (fg.solve_GN_rays if mode == "rays" else fg.solve_GN_calib)()
     got = np.stack([kfs[k].T_WC.data.cpu().numpy()[0] for k in range(6)])
-    np.testing.assert_allclose(got, g[f"{mode}_Twc"], atol=1e-5)
+    # SURVEY §8 a-note 6: the contract is 1e-5 against the fp64 truth of the same algorithm (the
+    # fp32 reference order itself sits 7-8e-6 from it on this ill-conditioned 6-KF fixture, see
+    # test_oracle.py); against the reference-glue golden the two fp32 roundings add up: 2e-5.
+    sig = (0.003, 10.0) if mode == "rays" else (1.0, 10.0)
+    Xs = g["Xs"] if mode == "rays" else O.backproject_constrain(g["Xs"], g["K"], (H, W))
+    p = O.ba_params(mode, sig[0], sig[1], 0.0, 1.5, K=g["K"], height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    ii2 = np.concatenate((g["ii"], g["jj"]))
+    jj2 = np.concatenate((g["jj"], g["ii"]))
+    T64, _, _ = O.gauss_newton_f64(mode, g["Twc0"], Xs, g["Cs"][..., 0], ii2, jj2, g["idx2"], g["valid2"][..., 0],
+                                   g["Q2"][..., 0], p, 10, 1e-8)
+    np.testing.assert_allclose(got, T64, atol=1e-5)
+    np.testing.assert_allclose(got, g[f"{mode}_Twc"], atol=2e-5)
 
 
 def test_sharded_split_api_single_process_equals_full(golden):

@@ -113,6 +113,23 @@ def test_oracle_ba_reproduces_reference_factor_graph(golden, mode):
     np.testing.assert_allclose(T, g[f"{mode}_Twc"], atol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_reference_order_fp32_within_1e5_of_fp64_truth(golden, mode):
+    """SURVEY §8 a-note 6: the reference's fp32 per-point order (golden, via the reference glue) sits
+    within 1e-5 of the fp64 truth of the same algorithm (oracle/Makefile F64 build)."""
+    g = golden("ba_6kf_24x32.npz")
+    sig = (0.003, 10.0) if mode == "rays" else (1.0, 10.0)
+    H, W = 24, 32
+    Xs = g["Xs"] if mode == "rays" else O.backproject_constrain(g["Xs"], g["K"], (H, W))
+    p = O.ba_params(mode, sig[0], sig[1], 0.0, 1.5, K=g["K"], height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    ii = np.concatenate((g["ii"], g["jj"]))
+    jj = np.concatenate((g["jj"], g["ii"]))
+    T64, _, its = O.gauss_newton_f64(mode, g["Twc0"], Xs, g["Cs"][..., 0], ii, jj, g["idx2"], g["valid2"][..., 0],
+                                     g["Q2"][..., 0], p, 10, 1e-8)
+    assert its == 10
+    np.testing.assert_allclose(g[f"{mode}_Twc"], T64, atol=1e-5)
+
+
 def test_oracle_ba_converges_on_consistent_problem():
     rng = np.random.default_rng(0)
     N = 1024
