@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define M3S_ABI_VERSION 2
+#define M3S_ABI_VERSION 3
 
 #define M3S_OK 0
 #define M3S_EINVAL -1  /* bad shape / argument (reference: TORCH_CHECK -> RuntimeError) */
@@ -158,6 +158,10 @@ typedef struct m3s_track_fuse_args {
   const float* Ckf;      /* (N) */
   float* Xk_out;         /* (N,3) fused X_canon (may alias Xk_canon: in place) */
   float* Ck_out;         /* (N)   fused C (may alias Ck_sum) */
+  const float* Cf;       /* (N)   frame C (for Cf_avg_out; nullable) */
+  float* Ck_avg_out;     /* (N)   fused C / Nk_new = keyframe.get_average_conf() (nullable) */
+  float* Cf_avg_out;     /* (N)   Cf / Nf = frame.get_average_conf() (nullable) */
+  float Nk_new, Nf;      /* keyframe N after this fusion, frame N (frame.py:83-84) */
 } m3s_track_fuse_args;
 
 typedef struct m3s_track_result {

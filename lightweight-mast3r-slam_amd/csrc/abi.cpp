@@ -28,8 +28,7 @@ hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*
                                  void*, int*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
-hipError_t m3s_launch_fuse(const void*, int, const float*, const float*, float*, float*, const float*, const float*,
-                           int, hipStream_t);
+hipError_t m3s_launch_fuse(const void*, int, const FuseArgs*, int, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
@@ -356,7 +355,23 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   hipStream_t s = (hipStream_t)stream;
   a.T_out = T_out_dev;
   const bool do_fuse = fuse && fuse->Xk_canon;
-  if (do_fuse) M3S_CHECK(fuse->Ck_sum && fuse->Xkf && fuse->Ckf, "track: fusion needs Ck_sum, Xkf, Ckf");
+  FuseArgs fa{};
+  if (do_fuse) {
+    M3S_CHECK(fuse->Ck_sum && fuse->Xkf && fuse->Ckf, "track: fusion needs Ck_sum, Xkf, Ckf");
+    M3S_CHECK(!fuse->Ck_avg_out || fuse->Nk_new > 0.0f, "track: Ck_avg_out needs Nk_new > 0");
+    M3S_CHECK(!fuse->Cf_avg_out || (fuse->Cf && fuse->Nf > 0.0f), "track: Cf_avg_out needs Cf and Nf > 0");
+    fa.X_in = fuse->Xk_canon;
+    fa.C_in = fuse->Ck_sum;
+    fa.Xkf = fuse->Xkf;
+    fa.Ckf = fuse->Ckf;
+    fa.X_out = fuse->Xk_out ? fuse->Xk_out : const_cast<float*>(fuse->Xk_canon);
+    fa.C_out = fuse->Ck_out ? fuse->Ck_out : const_cast<float*>(fuse->Ck_sum);
+    fa.Cf = fuse->Cf;
+    fa.Ck_avg = fuse->Ck_avg_out;
+    fa.Cf_avg = fuse->Cf_avg_out;
+    fa.Nk_new = fuse->Nk_new;
+    fa.Nf = fuse->Nf;
+  }
   HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
   {
     Span sp("track_setup", s);
@@ -374,10 +389,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     launched += chunk;
     // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
     // before the readback, it runs only if this batch finished the solve (done_chunk == chunk_id)
-    if (do_fuse)
-      HIP_TRY(m3s_launch_fuse(st, chunk_id, fuse->Xk_canon, fuse->Ck_sum, fuse->Xk_out ? fuse->Xk_out : (float*)fuse->Xk_canon,
-                              fuse->Ck_out ? fuse->Ck_out : (float*)fuse->Ck_sum, fuse->Xkf, fuse->Ckf, N, s),
-              "track fuse launch");
+    if (do_fuse) HIP_TRY(m3s_launch_fuse(st, chunk_id, &fa, N, s), "track fuse launch");
     HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
     HIP_TRY(hipStreamSynchronize(s), "track sync");
     if (hs.done || launched >= p.max_iters) break;

@@ -55,3 +55,17 @@ struct TrackArgs {
   TrackState* state;
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
 };
+
+// keyframe fusion (weighted_pointmap) + the match_info average confidences (frame.py:74-77, 83-84)
+struct FuseArgs {
+  const float* X_in;  // (N,3) keyframe X_canon
+  const float* C_in;  // (N)   keyframe C
+  const float* Xkf;   // (N,3) keyframe points in the frame's camera
+  const float* Ckf;   // (N)
+  float* X_out;       // (N,3) may alias X_in
+  float* C_out;       // (N)   may alias C_in
+  const float* Cf;    // (N)   frame C (nullable)
+  float* Ck_avg;      // (N)   C_out / Nk_new (nullable)
+  float* Cf_avg;      // (N)   Cf / Nf (nullable)
+  float Nk_new, Nf;
+};

@@ -475,9 +475,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
 // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77). Runs only if the
 // GN batch `chunk_id` finished with a pose (so it can be enqueued before the host reads the state
 // back). Out of place like the reference (new X_canon / C tensors); X_out may alias X_in.
-__global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id,
-                                                   const float* X_in, const float* C_in, float* X_out, float* C_out,
-                                                   const float* __restrict__ Xkf, const float* __restrict__ Ckf,
+__global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id, FuseArgs f,
                                                    int N) {
   if (!(st->done && st->done_chunk == chunk_id &&
         (st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)))
@@ -487,17 +485,19 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
   float T[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) T[c] = st->T[c];
-  const float X[3] = {Xkf[3 * (size_t)n], Xkf[3 * (size_t)n + 1], Xkf[3 * (size_t)n + 2]};
+  const float X[3] = {f.Xkf[3 * (size_t)n], f.Xkf[3 * (size_t)n + 1], f.Xkf[3 * (size_t)n + 2]};
   float Y[3];
   actSim3(T, X, Y);
-  const float c0 = C_in[n], c1 = Ckf[n];
+  const float c0 = f.C_in[n], c1 = f.Ckf[n];
   const float den = c0 + c1;
   float Xo[3];
 #pragma unroll
-  for (int k = 0; k < 3; k++) Xo[k] = (c0 * X_in[3 * (size_t)n + k] + c1 * Y[k]) / den;
+  for (int k = 0; k < 3; k++) Xo[k] = (c0 * f.X_in[3 * (size_t)n + k] + c1 * Y[k]) / den;
 #pragma unroll
-  for (int k = 0; k < 3; k++) X_out[3 * (size_t)n + k] = Xo[k];
-  C_out[n] = den;
+  for (int k = 0; k < 3; k++) f.X_out[3 * (size_t)n + k] = Xo[k];
+  f.C_out[n] = den;
+  if (f.Ck_avg != nullptr) f.Ck_avg[n] = den / f.Nk_new;  // keyframe.get_average_conf()
+  if (f.Cf_avg != nullptr) f.Cf_avg[n] = f.Cf[n] / f.Nf;  // frame.get_average_conf()
 }
 
 }  // namespace m3s
@@ -523,11 +523,9 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
   return hipGetLastError();
 }
 
-extern "C" hipError_t m3s_launch_fuse(const void* state, int chunk_id, const float* X_in, const float* C_in,
-                                      float* X_out, float* C_out, const float* Xkf, const float* Ckf, int N,
-                                      hipStream_t s) {
+extern "C" hipError_t m3s_launch_fuse(const void* state, int chunk_id, const FuseArgs* f, int N, hipStream_t s) {
   hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s,
-                     reinterpret_cast<const TrackState*>(state), chunk_id, X_in, C_in, X_out, C_out, Xkf, Ckf, N);
+                     reinterpret_cast<const TrackState*>(state), chunk_id, *f, N);
   return hipGetLastError();
 }
 

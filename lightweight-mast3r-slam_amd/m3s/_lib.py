@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # M3S_LIB: alternative build of the same library (kernel experiments); still the HIP library, no fallback
 LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libm3s.so")
 
-ABI_VERSION = 2  # include/m3s.h M3S_ABI_VERSION
+ABI_VERSION = 3  # include/m3s.h M3S_ABI_VERSION
 
 c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
 
@@ -45,7 +45,8 @@ class TrackInputs(ctypes.Structure):
 
 class TrackFuse(ctypes.Structure):
     _fields_ = [("Xk_canon", c_void_p), ("Ck_sum", c_void_p), ("Xkf", c_void_p), ("Ckf", c_void_p),
-                ("Xk_out", c_void_p), ("Ck_out", c_void_p)]
+                ("Xk_out", c_void_p), ("Ck_out", c_void_p), ("Cf", c_void_p), ("Ck_avg_out", c_void_p),
+                ("Cf_avg_out", c_void_p), ("Nk_new", c_float), ("Nf", c_float)]
 
 
 class TrackResult(ctypes.Structure):
@@ -113,7 +114,15 @@ def check(rc):
         raise RuntimeError(f"m3s error {rc}: {msg}")
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None):
+    """torch's current HIP stream on `device` (raw handle; no Stream object on the hot path)."""
+    if _RAW_STREAM is not None:
+        idx = device.index if isinstance(device, torch.device) and device.index is not None else (
+            device if isinstance(device, int) else torch.cuda.current_device())
+        return c_void_p(_RAW_STREAM(idx))
     return c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -69,6 +69,17 @@ def _host_K(K):
     return Kh
 
 
+def _as(t, dt=torch.float32):
+    """t as a contiguous dt tensor, without a dispatcher round trip when it already is one."""
+    if t is None or (t.dtype == dt and t.is_contiguous()):
+        return t
+    return t.to(dt).contiguous()
+
+
+def _dp(t):
+    return 0 if t is None else t.data_ptr()
+
+
 def frame_img_size(frame):
     """(H, W): ``frame.img.shape[-2:]`` for a reference Frame (tracker.py:47), ``img_size`` for m3s.frame."""
     size = getattr(frame, "img_size", None)
@@ -107,6 +118,19 @@ class FrameTracker:
 
     def reset_idx_f2k(self):
         self.idx_f2k = None
+
+    def _config(self, use_calib, img_size, K, max_iters):
+        """m3s_track_config, rebuilt only when the inputs that shape it change."""
+        cfg = self.cfg
+        kkey = None if (K is None or not use_calib) else (K.data_ptr(), K._version)
+        key = (use_calib, tuple(img_size), kkey, max_iters, tuple(cfg.items()))
+        if getattr(self, "_cfg_key", None) != key:
+            c = dict(cfg)
+            if max_iters is not None:
+                c["max_iters"] = max_iters
+            self._cfg_struct = _track_config(c, use_calib, img_size, K)
+            self._cfg_key = key
+        return self._cfg_struct
 
     # ------------------------------------------------------------------ fused track
     def track(self, frame):
@@ -157,53 +181,56 @@ class FrameTracker:
         new_kf = min(match_frac_k, unique_frac_f) < cfg["match_frac_thresh"]
         if new_kf:
             self.reset_idx_f2k()
-        return (new_kf, [keyframe.X_canon, keyframe.get_average_conf(), frame.X_canon, frame.get_average_conf(),
-                         Qkf, Qff], False)
+        if fuse_fused:  # C / N of both frames, written by the fuse kernel (frame.py:83-84)
+            Ck_avg, Cf_avg = self._avg
+        else:
+            Ck_avg, Cf_avg = keyframe.get_average_conf(), frame.get_average_conf()
+        return (new_kf, [keyframe.X_canon, Ck_avg, frame.X_canon, Cf_avg, Qkf, Qff], False)
 
     def _run_track(self, idx, valid, Xf, Cf, Nf, Qff, Xk, Ck, Nk, Qkf, T_WCf, T_WCk, use_calib, img_size, K,
                    fuse=None, direct=False, meas_k=None, valid_meas_k=None, max_iters=None):
         lib = _lib.load()
         dev = Xf.device
         _lib.require_cuda("track", Xf, Xk, Qff, valid)
-        cfg = dict(self.cfg)
-        if max_iters is not None:
-            cfg["max_iters"] = max_iters
-        tc = _track_config(cfg, use_calib, img_size, K)
+        tc = self._config(use_calib, img_size, K, max_iters)
         N = tc.H * tc.W
-        c = lambda t, dt=torch.float32: None if t is None else t.to(dt).contiguous()
+        c = _as
         Xf, Xk, Qff, Qkf, Cf, Ck = c(Xf), c(Xk), c(Qff), c(Qkf), c(Cf), c(Ck)
         idx = c(idx, torch.int64)
-        valid = valid.reshape(-1).to(torch.bool).contiguous()
+        valid = c(valid.reshape(-1), torch.bool)
         meas_k = c(meas_k)
-        valid_meas_k = None if valid_meas_k is None else valid_meas_k.reshape(-1).to(torch.bool).contiguous()
-        TWf = T_WCf.data.reshape(8).float().contiguous()
-        TWk = T_WCk.data.reshape(8).float().contiguous()
+        valid_meas_k = None if valid_meas_k is None else c(valid_meas_k.reshape(-1), torch.bool)
+        TWf = c(T_WCf.data.reshape(8))
+        TWk = c(T_WCk.data.reshape(8))
         for t in (Xf, Xk):
             if t is not None and t.numel() != 3 * N:
                 raise RuntimeError("track: pointmaps must have H*W points")
+        dp = _dp
         ins = _lib.TrackInputs(
-            idx_f2k=_lib.ptr(idx).value, valid_match=_lib.ptr(valid).value, Xf=_lib.ptr(Xf).value,
-            Cf=_lib.ptr(Cf).value, Nf=float(Nf or 1), Qff=_lib.ptr(Qff).value, Xk=_lib.ptr(Xk).value,
-            Ck=_lib.ptr(Ck).value, Nk=float(Nk or 1), Qkf=_lib.ptr(Qkf).value, T_WCf=_lib.ptr(TWf).value,
-            T_WCk=_lib.ptr(TWk).value, direct=1 if direct else 0, meas_k=_lib.ptr(meas_k).value,
-            valid_meas_k=_lib.ptr(valid_meas_k).value)
+            idx_f2k=dp(idx), valid_match=dp(valid), Xf=dp(Xf), Cf=dp(Cf), Nf=float(Nf or 1), Qff=dp(Qff),
+            Xk=dp(Xk), Ck=dp(Ck), Nk=float(Nk or 1), Qkf=dp(Qkf), T_WCf=dp(TWf), T_WCk=dp(TWk),
+            direct=1 if direct else 0, meas_k=dp(meas_k), valid_meas_k=dp(valid_meas_k))
         fz = _lib.TrackFuse()
         keep = []
-        self._fused = None
+        self._fused = self._avg = None
         if fuse is not None:  # out of place like frame.py:75-76 (earlier holders keep the old tensors)
             kf, Xkf, Ckf = fuse
             Xin, Cin = c(kf.X_canon), c(kf.C)
             Xkf_c, Ckf_c = c(Xkf), c(Ckf)
             Xo, Co = torch.empty_like(Xin), torch.empty_like(Cin)
+            Cka, Cfa = torch.empty_like(Cin), torch.empty_like(Cf)
             keep += [Xin, Cin, Xkf_c, Ckf_c]
             self._fused = (Xo, Co)
-            fz = _lib.TrackFuse(Xk_canon=_lib.ptr(Xin).value, Ck_sum=_lib.ptr(Cin).value, Xkf=_lib.ptr(Xkf_c).value,
-                                Ckf=_lib.ptr(Ckf_c).value, Xk_out=_lib.ptr(Xo).value, Ck_out=_lib.ptr(Co).value)
+            self._avg = (Cka, Cfa)
+            fz = _lib.TrackFuse(Xk_canon=dp(Xin), Ck_sum=dp(Cin), Xkf=dp(Xkf_c), Ckf=dp(Ckf_c), Xk_out=dp(Xo),
+                                Ck_out=dp(Co), Cf=dp(Cf), Ck_avg_out=dp(Cka), Cf_avg_out=dp(Cfa),
+                                Nk_new=float(kf.N + 1), Nf=float(Nf or 1))
         T_out = torch.empty(16, dtype=torch.float32, device=dev)
         res = _lib.TrackResult()
         ws = _lib.workspace("track", lib.m3s_track_workspace_size(N), dev)
         _lib.check(lib.m3s_track(ctypes.byref(ins), ctypes.byref(tc), ctypes.byref(fz), int(self.first_chunk),
-                                 _lib.ptr(T_out), ctypes.byref(res), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)))
+                                 T_out.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(),
+                                 _lib.stream_ptr(dev)))
         self.last_result = res
         if not direct:  # next frame: enqueue as many GN launches as this one needed (+1) before reading back
             self.first_chunk = max(2, min(int(tc.max_iters), res.iters + 1))
