@@ -243,10 +243,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # M3S_BENCH_DEVICE / M3S_DIST_BACKEND: rehearsal of the N-rank path on a 1-GPU box (all ranks on
+    # one device over gloo); the driver's multi-GPU runs use one GPU per rank over RCCL ("nccl").
+    ndev = os.environ.get("M3S_BENCH_DEVICE")
+    local_dev = int(ndev) if ndev is not None else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("M3S_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import __graft_entry__  # noqa: F401  (sys.path)
 
     elapsed, kern, gn_iters, N = bench_tracking(args, rank, world, dev)
