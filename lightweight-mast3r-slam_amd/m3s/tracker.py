@@ -138,7 +138,9 @@ class FrameTracker:
         keyframe = self.keyframes.last_keyframe()
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = mast3r_match_asymmetric(
             self.model, frame, keyframe, idx_i2j_init=self.idx_f2k)
-        self.idx_f2k = idx_f2k.clone()
+        # tracker.py:45 clones; the fused matcher returns a fresh tensor that nothing writes to, so the
+        # warm-start reference keeps it without a copy
+        self.idx_f2k = idx_f2k
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
         frame.update_pointmap(Xff, Cff)
