@@ -470,6 +470,7 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
   M3S_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "ba: bad shard range");
+  M3S_CHECK((int64_t)(Kp - 1) * 7 <= 8192, "ba: at most 1171 poses (dense system held in LDS by the back solve)");
   if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
                                 "ba calib: height*width must equal the points per keyframe");
   if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");

@@ -27,7 +27,6 @@
 namespace m3s {
 
 #define BA_NSUM 36
-#define CH_NB 64
 
 // ------------------------------------------------------------------------------------------
 // linearisation
@@ -283,8 +282,14 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 }
 
 // ------------------------------------------------------------------------------------------
-// dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1
+// dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1.
+// Panels of PNB = 32 columns: the serial work per panel (diagonal factorisation, one wave) grows
+// with PNB^2 per lane, so a narrow panel keeps the critical path short; the trailing update runs
+// on 64x64 tiles of depth PNB.
 // ------------------------------------------------------------------------------------------
+#define PNB 32
+#define UT 64
+
 // lanes of one wave exchanging data through LDS: a compiler memory barrier (the hardware returns a
 // wave's LDS accesses in order)
 __device__ __forceinline__ void wave_sync() {
@@ -299,26 +304,12 @@ __device__ __forceinline__ double bcast_lane(double v, int src) {
   return *reinterpret_cast<double*>(&x);
 }
 
-// Stage a 64-row block of H (rows r0.., columns k0..k0+63) into LDS with coalesced loads (lane =
-// column), all loads of a 32-row batch in flight before the stores.
-__device__ __forceinline__ void stage_rows(const double* __restrict__ H, int n, int r0, int nr, int k0, int kb,
-                                           double (*S)[CH_NB + 1], int lane) {
-  const int lc = min(lane, kb - 1);
-  for (int t0 = 0; t0 < CH_NB; t0 += 32) {
-    double v[32];
-#pragma unroll
-    for (int u = 0; u < 32; u++) v[u] = H[(size_t)(r0 + min(t0 + u, nr - 1)) * n + k0 + lc];
-#pragma unroll
-    for (int u = 0; u < 32; u++) S[t0 + u][lane] = (t0 + u < nr && lane < kb) ? v[u] : 0.0;
-  }
-}
-
 // Right-looking column step J of the register-row diagonal factorisation: pivot and column
-// multipliers broadcast with readlane (no LDS round trip), rank-1 update of the lane's own row.
-// Rows/columns >= kb are padded with the identity, so every step is valid and the padding inert.
+// multipliers broadcast with readlane, rank-1 update of the lane's own row. Rows/columns >= kb are
+// padded with the identity, so every step is valid and the padding stays inert.
 template <int J>
-__device__ __forceinline__ void diag_step(double (&r)[CH_NB], int lane, bool& bad) {
-  if constexpr (J < CH_NB) {
+__device__ __forceinline__ void diag_step(double (&r)[PNB], int lane, bool& bad) {
+  if constexpr (J < PNB) {
     double d = bcast_lane(r[J], J);
     if (!(d > 0.0)) {
       bad = true;
@@ -331,99 +322,128 @@ __device__ __forceinline__ void diag_step(double (&r)[CH_NB], int lane, bool& ba
     const double l = r[J] * inv;
     r[J] = lane == J ? sj : (lane > J ? l : r[J]);
 #pragma unroll
-    for (int c = J + 1; c < CH_NB; c++) r[c] -= l * bcast_lane(l, c);
+    for (int c = J + 1; c < PNB; c++) r[c] -= l * bcast_lane(l, c);
     diag_step<J + 1>(r, lane, bad);
   }
 }
 
-// 64x64 diagonal block by one wave: lane i keeps row i in registers (static indices: the steps are
-// compile-time), ~2k FMAs + 4k readlanes per lane, no barriers. Also writes L11^T to Lt for the
-// panel solve (scalar-loadable there).
+// PNBxPNB diagonal block by one wave (lanes 0..31 = rows, in registers; static indices because the
+// steps are compile-time). Also writes L11^T to Lt for the panel solve (scalar-loadable there).
 __global__ void __launch_bounds__(64) chol_diag_kernel(double* __restrict__ H, double* __restrict__ Lt, int n, int k0,
                                                        int* __restrict__ info, const int* __restrict__ done) {
   if (*done) return;
-  const int kb = min(CH_NB, n - k0);
-  __shared__ double S[CH_NB][CH_NB + 1];
+  const int kb = min(PNB, n - k0);
+  __shared__ double S[PNB][PNB + 1];
   const int lane = threadIdx.x;
-  stage_rows(H, n, k0, kb, k0, kb, S, lane);
-  wave_sync();
-  double r[CH_NB];
+  const int li = min(lane, PNB - 1);
+  {
+    double v[PNB];
 #pragma unroll
-  for (int c = 0; c < CH_NB; c++) r[c] = (lane < kb && c < kb) ? S[lane][c] : (c == lane ? 1.0 : 0.0);
+    for (int t = 0; t < PNB; t++) v[t] = H[(size_t)(k0 + min(t, kb - 1)) * n + k0 + min(li, kb - 1)];
+    if (lane < PNB)
+#pragma unroll
+      for (int t = 0; t < PNB; t++) S[t][lane] = (t < kb && lane < kb && lane <= t) ? v[t] : 0.0;
+  }
+  wave_sync();
+  double r[PNB];
+#pragma unroll
+  for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
   bool bad = false;
   diag_step<0>(r, lane, bad);
   if (bad && lane == 0) *info = 1;
   wave_sync();
+  if (lane < PNB)
 #pragma unroll
-  for (int c = 0; c < CH_NB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
+    for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
   wave_sync();
-  for (int t = 0; t < kb; t++)  // coalesced write-back of the lower triangle (lane = column)
-    if (lane <= t) H[(size_t)(k0 + t) * n + k0 + lane] = S[t][lane];
-  for (int t = 0; t < CH_NB; t++) Lt[t * CH_NB + lane] = S[lane][t];  // Lt[j][k] = L[k][j] (padded)
-}
-
-// Right-looking step J of the register-row forward substitution: x_J /= L_JJ, then fold x_J into
-// the later columns with column J of L11 — uniform addresses of a restrict-const buffer, so the
-// compiler reads them with scalar loads (SGPR operands, no LDS).
-template <int J>
-__device__ __forceinline__ void trsm_step(double (&x)[CH_NB], const double* __restrict__ Lt) {
-  if constexpr (J < CH_NB) {
-    x[J] /= Lt[J * CH_NB + J];
-#pragma unroll
-    for (int k = J + 1; k < CH_NB; k++) x[k] -= x[J] * Lt[J * CH_NB + k];
-    trsm_step<J + 1>(x, Lt);
+  if (lane < PNB) {
+    for (int t = 0; t < kb; t++)  // coalesced write-back of the lower triangle (lane = column)
+      if (lane <= t) H[(size_t)(k0 + t) * n + k0 + lane] = S[t][lane];
+    for (int t = 0; t < PNB; t++) Lt[t * PNB + lane] = S[lane][t];  // Lt[j][k] = L[k][j] (padded)
   }
 }
 
-// rows r in [k0+kb, n] (row n = rhs): L21 = A21 L11^-T. One wave per 64 rows, lane = row in
-// registers; L11^T from the diagonal kernel (padding: identity).
+// Right-looking step J of the register-row forward substitution: x_J *= 1/L_JJ, then fold x_J into
+// the later columns with column J of L11 (= row J of Lt, staged in LDS: broadcast reads; no compiler
+// barrier here — a memory clobber inside the unrolled steps makes the allocator spill x[]).
+template <int J>
+__device__ __forceinline__ void trsm_step(double (&x)[PNB], const double (*Ls)[PNB + 2]) {
+  if constexpr (J < PNB) {
+    x[J] *= Ls[J][PNB];  // reciprocal of the pivot, stored after the row
+#pragma unroll
+    for (int k0 = J + 1; k0 < PNB; k0 += 8) {
+#pragma unroll
+      for (int k = k0; k < (k0 + 8 < PNB ? k0 + 8 : PNB); k++) x[k] -= x[J] * Ls[J][k];
+    }
+    trsm_step<J + 1>(x, Ls);
+  }
+}
+
+// rows r in [k0+kb, n] (row n = rhs): L21 = A21 L11^-T. One wave per 64 rows, lane = row, its PNB
+// panel entries in registers; L11^T (from the diagonal kernel) staged in LDS with the pivots'
+// reciprocals.
 __global__ void __launch_bounds__(64) chol_trsm_kernel(double* __restrict__ H, const double* __restrict__ Lt, int n,
                                                        int k0, const int* __restrict__ done) {
   if (*done) return;
-  const int kb = min(CH_NB, n - k0);
-  __shared__ double X[CH_NB][CH_NB + 1];
+  const int kb = min(PNB, n - k0);
   const int lane = threadIdx.x;
-  const int r0 = k0 + kb + blockIdx.x * CH_NB;
-  const int nr = min(CH_NB, n + 1 - r0);
-  stage_rows(H, n, r0, nr, k0, kb, X, lane);
-  wave_sync();
-  double x[CH_NB];
+  __shared__ double Ls[PNB][PNB + 2];
+  {
+    double v[PNB * PNB / 64];
 #pragma unroll
-  for (int c = 0; c < CH_NB; c++) x[c] = X[lane][c];
-  trsm_step<0>(x, Lt);
-  wave_sync();
+    for (int u = 0; u < PNB * PNB / 64; u++) v[u] = Lt[lane + 64 * u];
 #pragma unroll
-  for (int c = 0; c < CH_NB; c++) X[lane][c] = x[c];
+    for (int u = 0; u < PNB * PNB / 64; u++) {
+      const int t = lane + 64 * u;
+      Ls[t / PNB][t % PNB] = v[u];
+    }
+  }
   wave_sync();
-  for (int t = 0; t < nr; t++)
-    if (lane < kb) H[(size_t)(r0 + t) * n + k0 + lane] = X[t][lane];
+  if (lane < PNB) Ls[lane][PNB] = 1.0 / Ls[lane][lane];
+  const int r = k0 + kb + blockIdx.x * 64 + lane;
+  const int rr = min(r, n);
+  double* row = H + (size_t)rr * n + k0;
+  double x[PNB];
+#pragma unroll
+  for (int c = 0; c < PNB; c++) x[c] = c < kb ? row[min(c, kb - 1)] : 0.0;
+  wave_sync();
+  trsm_step<0>(x, Ls);
+  if (r <= n) {
+    // branch-free stores (a per-column `if (c < kb)` makes the allocator spill x[]): columns past
+    // kb rewrite column kb-1 with its own value
+    double keep = x[0];  // x[kb - 1], selected without dynamic indexing
+#pragma unroll
+    for (int c = 1; c < PNB; c++) keep = (c == kb - 1) ? x[c] : keep;
+#pragma unroll
+    for (int c = 0; c < PNB; c++) row[min(c, kb - 1)] = c < kb ? x[c] : keep;
+  }
 }
 
-// trailing update A22 -= L21 L21^T over 64x64 lower tiles; rows [s, n], cols [s, n-1], s = k0+kb
+// trailing update A22 -= L21 L21^T over UTxUT lower tiles, depth kb <= PNB; rows [s, n], cols [s, n-1]
 __global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H, int n, int k0,
                                                           const int* __restrict__ done) {
   if (*done) return;
-  const int kb = min(CH_NB, n - k0);
+  const int kb = min(PNB, n - k0);
   const int s = k0 + kb;
   const int ti = blockIdx.x, tj = blockIdx.y;
   if (tj > ti) return;
-  const int r0 = s + ti * CH_NB, c0 = s + tj * CH_NB;
+  const int r0 = s + ti * UT, c0 = s + tj * UT;
   if (c0 >= n) return;
-  const int nr = min(CH_NB, n + 1 - r0), nc = min(CH_NB, n - c0);
-  __shared__ double A[CH_NB][CH_NB + 1];
-  __shared__ double B[CH_NB][CH_NB + 1];
-  {  // 16 + 16 per lane, branch-free, all loads issued before the LDS stores
-    double av[16], bv[16];
+  const int nr = min(UT, n + 1 - r0), nc = min(UT, n - c0);
+  __shared__ double A[UT][PNB + 1];
+  __shared__ double B[UT][PNB + 1];
+  {  // 8 + 8 per lane, branch-free, all loads issued before the LDS stores
+    double av[8], bv[8];
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / CH_NB, k = t % CH_NB;
+    for (int u = 0; u < 8; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / PNB, k = t % PNB;
       const int kc = min(k, kb - 1);
       av[u] = H[(size_t)(r0 + min(i, nr - 1)) * n + k0 + kc];
       bv[u] = H[(size_t)(c0 + min(i, nc - 1)) * n + k0 + kc];
     }
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / CH_NB, k = t % CH_NB;
+    for (int u = 0; u < 8; u++) {
+      const int t = threadIdx.x + 256 * u, i = t / PNB, k = t % PNB;
       A[i][k] = (i < nr && k < kb) ? av[u] : 0.0;
       B[i][k] = (i < nc && k < kb) ? bv[u] : 0.0;
     }
@@ -435,7 +455,8 @@ __global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H
   for (int x = 0; x < 4; x++)
 #pragma unroll
     for (int y = 0; y < 4; y++) acc[x][y] = 0.0;
-  for (int k = 0; k < kb; k++) {
+#pragma unroll 8
+  for (int k = 0; k < PNB; k++) {
     double av[4], bv[4];
 #pragma unroll
     for (int x = 0; x < 4; x++) av[x] = A[ty + 16 * x][k];
@@ -460,51 +481,53 @@ __global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H
   }
 }
 
-// backward substitution L^T x = y for the panel at k0 (called for panels in reverse order):
-// the already-solved tail is folded in by a 4x64-lane column GEMV, then wave 0 back-solves the
-// 64x64 diagonal block with x broadcast by lane shuffles.
-__global__ void __launch_bounds__(256) chol_back_kernel(const double* __restrict__ H, double* __restrict__ x, int n,
-                                                        int k0, const int* __restrict__ done) {
+// Whole back substitution L^T x = y (y = row n after the factorisation) in ONE block: 64-column
+// panels from the end; per panel the solved tail is folded in by a 16-group x 64-column GEMV, then
+// wave 0 back-solves the 64x64 diagonal block with lane shuffles. x stays in LDS (n <= 8192).
+#define BK_NB 64
+__global__ void __launch_bounds__(1024) chol_back_all_kernel(const double* __restrict__ H, double* __restrict__ xg,
+                                                             int n, const int* __restrict__ done) {
   if (*done) return;
-  const int kb = min(CH_NB, n - k0);
-  __shared__ double part[4][CH_NB];
-  __shared__ double Ld[CH_NB][CH_NB + 1];
-  const int c = threadIdx.x % CH_NB, g = threadIdx.x / CH_NB;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // independent partial sums: 4 row loads in flight per lane
-  if (c < kb) {
-    int r = k0 + kb + g;
-    for (; r + 12 < n; r += 16) {
+  __shared__ double xs[8192];
+  __shared__ double part[16][BK_NB];
+  __shared__ double Ld[BK_NB][BK_NB + 1];
+  const int c = threadIdx.x % BK_NB, g = threadIdx.x / BK_NB;
+  for (int k0 = ((n - 1) / BK_NB) * BK_NB; k0 >= 0; k0 -= BK_NB) {
+    const int kb = min(BK_NB, n - k0);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (c < kb) {
+      int r = k0 + kb + g;
+      for (; r + 48 < n; r += 64) {
 #pragma unroll
-      for (int u = 0; u < 4; u++) acc[u] += H[(size_t)(r + 4 * u) * n + k0 + c] * x[r + 4 * u];
+        for (int u = 0; u < 4; u++) acc[u] += H[(size_t)(r + 16 * u) * n + k0 + c] * xs[r + 16 * u];
+      }
+      for (; r < n; r += 16) acc[0] += H[(size_t)r * n + k0 + c] * xs[r];
     }
-    for (; r < n; r += 4) acc[0] += H[(size_t)r * n + k0 + c] * x[r];
-  }
-  part[g][c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  {
-    double lv[16];
+    part[g][c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    for (int t = threadIdx.x; t < BK_NB * BK_NB; t += 1024) {
+      const int i = t / BK_NB, j = t % BK_NB;
+      Ld[i][j] = (i < kb && j <= i) ? H[(size_t)(k0 + i) * n + k0 + j] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      double y = 0.0;
+      if (lane < kb) {
+        double sp = 0.0;
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / CH_NB, j = t % CH_NB;
-      lv[u] = H[(size_t)(k0 + min(i, kb - 1)) * n + k0 + min(j, kb - 1)];
+        for (int q = 0; q < 16; q++) sp += part[q][lane];
+        y = H[(size_t)n * n + k0 + lane] - sp;
+      }
+      for (int cc = kb - 1; cc >= 0; cc--) {
+        const double xc = __shfl(y, cc, 64) / Ld[cc][cc];
+        if (lane == cc) y = xc;
+        if (lane < cc) y -= Ld[cc][lane] * xc;
+      }
+      if (lane < kb) xs[k0 + lane] = y;
     }
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / CH_NB, j = t % CH_NB;
-      Ld[i][j] = (i < kb && j <= i) ? lv[u] : 0.0;
-    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    double y = 0.0;
-    if (lane < kb) y = H[(size_t)n * n + k0 + lane] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
-    for (int cc = kb - 1; cc >= 0; cc--) {
-      const double xc = __shfl(y, cc, 64) / Ld[cc][cc];
-      if (lane == cc) y = xc;
-      if (lane < cc) y -= Ld[cc][lane] * xc;
-    }
-    if (lane < kb) x[k0 + lane] = y;
-  }
+  for (int i = threadIdx.x; i < n; i += 1024) xg[i] = xs[i];
 }
 
 // dx = -x (or 0 when the factorisation failed), poses k >= 1 retracted, |dx| early exit.
@@ -559,19 +582,19 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
   if (n > 0) {
     if (hipMemsetAsync(a->H, 0, sizeof(double) * (size_t)(n + 1) * n, s) != hipSuccess) return hipGetLastError();
     hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows), dim3(64), 0, s, *a, n, nblocks);
-    for (int k0 = 0; k0 < n; k0 += CH_NB) {
-      const int kb = n - k0 < CH_NB ? n - k0 : CH_NB;
+    for (int k0 = 0; k0 < n; k0 += PNB) {
+      const int kb = n - k0 < PNB ? n - k0 : PNB;
       hipLaunchKernelGGL(m3s::chol_diag_kernel, dim3(1), dim3(64), 0, s, a->H, a->Lt, n, k0, a->info, a->done);
       const int rows = n + 1 - (k0 + kb);
       if (rows > 0) {
-        const int tr = (rows + CH_NB - 1) / CH_NB;
-        hipLaunchKernelGGL(m3s::chol_trsm_kernel, dim3(tr), dim3(64), 0, s, a->H, a->Lt, n, k0, a->done);
-        const int tc = (n - (k0 + kb) + CH_NB - 1) / CH_NB;
+        hipLaunchKernelGGL(m3s::chol_trsm_kernel, dim3((rows + 63) / 64), dim3(64), 0, s, a->H, a->Lt, n, k0,
+                           a->done);
+        const int tr = (rows + UT - 1) / UT;
+        const int tc = (n - (k0 + kb) + UT - 1) / UT;
         if (tc > 0) hipLaunchKernelGGL(m3s::chol_update_kernel, dim3(tr, tc), dim3(256), 0, s, a->H, n, k0, a->done);
       }
     }
-    for (int k0 = ((n - 1) / CH_NB) * CH_NB; k0 >= 0; k0 -= CH_NB)
-      hipLaunchKernelGGL(m3s::chol_back_kernel, dim3(1), dim3(256), 0, s, a->H, a->x, n, k0, a->done);
+    hipLaunchKernelGGL(m3s::chol_back_all_kernel, dim3(1), dim3(1024), 0, s, a->H, a->x, n, a->done);
   }
   hipLaunchKernelGGL(m3s::ba_retr_kernel, dim3(1), dim3(256), 0, s, *a, K, n, delta_thresh);
   return hipGetLastError();
