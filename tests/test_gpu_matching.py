@@ -121,6 +121,33 @@ def test_fused_match_vs_oracle_batched(shape):
     assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
 
 
+def test_fused_match_scattered_warm_start_vs_oracle():
+    """A random warm start scatters the LM results, so many refine centres fall outside their tile's
+    LDS window: exercises the deferred-outlier list + wave-per-pixel kernel (refine.hip) against the
+    oracle's sequential scan, and the in-place cooperative path through the reference op."""
+    from m3s.matching import match
+    from m3s.synthetic import make_pair
+
+    H, W = 96, 128
+    P = make_pair(H, W, seed=21)
+    X11, X21 = P["X"][:1].numpy(), P["X"][1:].numpy()
+    D11, D21 = P["D"][:1].numpy(), P["D"][1:].numpy()
+    init = np.random.default_rng(3).integers(0, H * W, size=(1, H * W)).astype(np.int64)
+    ref_idx, ref_valid = O.match(X11, X21, D11, D21, idx_init=init)
+    idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21), _dev(init))
+    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-3
+    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
+    # reference op on the same scattered centres: bit-exact c10::Half refine
+    rays, pts, p_init = O.prep_for_iter_proj(X11, X21, init)
+    p_new, _ = O.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)
+    p1 = p_new.astype(np.int64)
+    ref = O.refine_matches(D11, D21.reshape(1, H * W, -1), p1, 3, 5)
+    import mast3r_slam_backends as B
+
+    (got,) = B.refine_matches(_dev(D11).half(), _dev(D21.reshape(1, H * W, -1)).half(), _dev(p1), 3, 5)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
 def test_fused_match_full_size_properties():
     """512x512 (BASELINE configs[0] shape): properties that do not need the oracle at full size."""
     from m3s.matching import match
