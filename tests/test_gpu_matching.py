@@ -121,6 +121,26 @@ def test_fused_match_vs_oracle_batched(shape):
     assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
 
 
+@pytest.mark.parametrize("shape,dmax", [((2, 50, 70), 5), ((1, 40, 96), 3), ((1, 64, 64), 8), ((1, 33, 47), 1)])
+def test_fused_match_ragged_and_dilations_vs_oracle(shape, dmax):
+    """Partial refine tiles (H % 8, W % 32 != 0), batch > 1 and every dilation specialisation."""
+    from m3s.config import config
+    from m3s.matching import match
+    from m3s.synthetic import make_pair
+
+    B, H, W = shape
+    config["matching"]["dilation_max"] = dmax
+    Ps = [make_pair(H, W, seed=30 + b) for b in range(B)]
+    X11 = np.stack([p["X"][0].numpy() for p in Ps])
+    X21 = np.stack([p["X"][1].numpy() for p in Ps])
+    D11 = np.stack([p["D"][0].numpy() for p in Ps])
+    D21 = np.stack([p["D"][1].numpy() for p in Ps])
+    ref_idx, ref_valid = O.match(X11, X21, D11, D21, dilation_max=dmax)
+    idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21))
+    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-3
+    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
+
+
 def test_fused_match_scattered_warm_start_vs_oracle():
     """A random warm start scatters the LM results, so many refine centres fall outside their tile's
     LDS window: exercises the deferred-outlier list + wave-per-pixel kernel (refine.hip) against the

@@ -49,6 +49,8 @@ def test_track_matches_reference(golden, mode):
     np.testing.assert_allclose(kf.C.cpu().numpy(), g[f"{mode}_kf_C"], atol=1e-5)
     assert kf.N == 2
     assert len(info) == 6
+    # match_info average confidences (fuse kernel outputs) == C / N (frame.py:83-84), exactly
+    assert torch.equal(info[1], kf.C / kf.N) and torch.equal(info[3], frame.C / frame.N)
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib"])
@@ -105,3 +107,67 @@ def test_track_full_size_converges_to_ground_truth():
     assert np.abs(T[:3] - T_gt[:3]).max() < 2e-3
     assert abs(T[7] - T_gt[7]) < 2e-3
     assert abs(abs(float(np.dot(T[3:7], T_gt[3:7]))) - 1.0) < 1e-5
+
+
+def _mode_cfg(key, value):
+    from m3s.config import config
+
+    config["tracking"][key] = value
+
+
+def test_track_cholesky_failure_returns_reloc(golden):
+    """tracker.py:84-89: a failed factorisation (here: no valid residual, H = 0) -> (False, [], True)."""
+    from m3s.tracker import FrameTracker
+
+    g = golden("tracking_48x64.npz")
+    kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+    _mode_cfg("min_match_frac", 0.0)
+    _mode_cfg("Q_conf", 1e9)
+    X0 = kf.X_canon.clone()
+    tr = FrameTracker(model, kfs, "cuda")
+    assert tr.track(frame) == (False, [], True)
+    assert torch.equal(kf.X_canon, X0) and kf.N == 1
+
+
+def test_opt_pose_raises_on_cholesky_failure(golden):
+    """torch.linalg.cholesky raises on a singular H (tracker.py:168): so does the direct surface."""
+    from m3s.sim3 import Sim3
+    from m3s.tracker import FrameTracker
+
+    g = golden("optpose_32x48.npz")
+    d = lambda k: torch.from_numpy(g[k]).cuda()
+    tr = FrameTracker(None, None, "cuda")
+    with pytest.raises(RuntimeError, match="cholesky"):
+        tr.opt_pose_ray_dist_sim3(d("Xf"), d("Xk"), Sim3(d("T_WCf")), Sim3(d("T_WCk")), d("Qk"),
+                                  torch.zeros_like(d("valid")))
+
+
+def test_track_max_iters_still_updates(golden):
+    """max_iters reached without convergence: the pose and the fusion are still applied (tracker.py:76-101)."""
+    from m3s import _lib
+    from m3s.tracker import FrameTracker
+
+    g = golden("tracking_48x64.npz")
+    kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+    _mode_cfg("max_iters", 1)
+    tr = FrameTracker(model, kfs, "cuda")
+    new_kf, info, reloc = tr.track(frame)
+    assert not reloc and tr.last_result.iters == 1 and tr.last_result.status == _lib.TRACK_MAX_ITERS
+    assert kf.N == 2 and len(info) == 6
+
+
+def test_track_recent_filtering_replaces_keyframe(golden):
+    """filtering_mode 'recent' (frame.py:59-62) takes the update_pointmap path: X = T_CkCf.act(Xkf), N = 1."""
+    from m3s.sim3 import Sim3
+    from m3s.tracker import FrameTracker
+
+    g = golden("tracking_48x64.npz")
+    kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+    _mode_cfg("filtering_mode", "recent")
+    tr = FrameTracker(model, kfs, "cuda")
+    new_kf, info, reloc = tr.track(frame)
+    assert not reloc
+    T_CkCf = Sim3(kf.T_WC.data).inv() * frame.T_WC
+    Xkf = torch.from_numpy(g["X"][1].reshape(-1, 3)).cuda()
+    np.testing.assert_allclose(kf.X_canon.cpu().numpy(), T_CkCf.act(Xkf).cpu().numpy(), atol=2e-5, rtol=1e-5)
+    assert kf.N == 1 and kf.N_updates == 2
