@@ -100,7 +100,10 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
     const float ci = Ci_base[ind];
     const float cj = Cj_base[k];
     bool valid = vm && (q > p.Q_thresh) && (ci > p.C_thresh) && (cj > p.C_thresh);
-    const float sqq = sqrtf(q);
+    // hardware sqrt/rsq/rcp (<= 1 ulp) instead of the correctly rounded sequences: the rows are
+    // VALU-bound here and the products are formed in fp64 afterwards; parity is checked against
+    // the fp64 truth (1e-5)
+    const float sqq = __builtin_amdgcn_sqrtf(q);
     if constexpr (MODE == BA_MODE_POINTS) {
       const float err[3] = {Y[0] - Xi[0], Y[1] - Xi[1], Y[2] - Xi[2]};
       const float sw = valid ? p.inv_a * sqq : 0.0f;
@@ -112,17 +115,18 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       acc_local<0b1101010>(L, v, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
       acc_local<0b1011100>(L, v, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
     } else if constexpr (MODE == BA_MODE_RAYS) {
-      const float n1i = sqrtf(Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2]);
-      const float n1i_inv = 1.0f / n1i;
+      const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+      const float n1i_inv = __builtin_amdgcn_rsqf(n2i);
+      const float n1i = n2i * n1i_inv;
       const float n2j = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
-      const float n1j = sqrtf(n2j);
-      const float n1j_inv = 1.0f / n1j;
+      const float n1j_inv = __builtin_amdgcn_rsqf(n2j);
+      const float n1j = n2j * n1j_inv;
       const float rj[3] = {n1j_inv * Y[0], n1j_inv * Y[1], n1j_inv * Y[2]};
       const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1], rj[2] - n1i_inv * Xi[2], n1j - n1i};
       const float swr = valid ? p.inv_a * sqq : 0.0f;
       const float swd = valid ? p.inv_b * sqq : 0.0f;
       const float wr = swr * swr, wd = swd * swd;
-      const float n3 = n1j_inv / n2j;
+      const float n3 = n1j_inv * __builtin_amdgcn_rcpf(n2j);
       const float dxx = n1j_inv - Y[0] * Y[0] * n3;
       const float dyy = n1j_inv - Y[1] * Y[1] * n3;
       const float dzz = n1j_inv - Y[2] * Y[2] * n3;
@@ -138,11 +142,12 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       acc_local<0b0011111>(L, v, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
       acc_local<0b1000111>(L, v, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
-      const int u_t = (int)(ind % p.W), v_t = (int)(ind / p.W);
+      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division instead of 64-bit
+      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
       const bool valid_z = (Y[2] > p.z_eps) && (Xi[2] > p.z_eps);
-      const float zj_inv = valid_z ? 1.0f / Y[2] : 0.0f;
-      const float zj_log = valid_z ? logf(Y[2]) : 0.0f;
-      const float zi_log = valid_z ? logf(Xi[2]) : 0.0f;
+      const float zj_inv = valid_z ? __builtin_amdgcn_rcpf(Y[2]) : 0.0f;
+      const float zj_log = valid_z ? __logf(Y[2]) : 0.0f;
+      const float zi_log = valid_z ? __logf(Xi[2]) : 0.0f;
       const float xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
       const float u = p.fx * xz + p.cx, vv = p.fy * yz + p.cy;
       const bool valid_u = (u > (float)p.pixel_border) && (u < (float)(p.W - 1 - p.pixel_border));
