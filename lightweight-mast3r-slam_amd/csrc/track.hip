@@ -123,13 +123,15 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
       rec[0] = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
       rec[1] = make_float4(di * Xk[1], di * Xk[2], d, sq);
     } else {  // calib: constrain_points_to_ray at pixel idx, meas_k = [u_n, v_n, log z_k]
-      const float uf = (float)(i % p.W), vf = (float)(i / p.W);
+      const int i32 = (int)i, vi = i32 / p.W;  // 32-bit: i < H*W
+      const float uf = (float)(i32 - vi * p.W), vf = (float)vi;
       const float zf = Xf[2];
       const float xc = zf * ((uf - p.cx) / p.fx);
       const float yc = zf * ((vf - p.cy) / p.fy);
       const float zk = Xk[2];
       const bool vmeas = zk > p.depth_eps;
-      const float un = (float)(n % p.W), vn = (float)(n / p.W);
+      const int vnn = n / p.W;
+      const float un = (float)(n - vnn * p.W), vn = (float)vnn;
       rec[0] = make_float4(xc, yc, zf, vmeas ? un : 0.0f);
       rec[1] = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
     }
