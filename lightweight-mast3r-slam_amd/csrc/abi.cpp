@@ -445,7 +445,7 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   a->rhs_ent = c.take<int>((size_t)2 * E);
   a->H = c.take<double>((size_t)(n + 1) * std::max(n, 1));
   a->x = c.take<double>(std::max(n, 1));
-  a->Lt = c.take<double>(64 * 64);
+  a->Lt = c.take<double>((size_t)((std::max(n, 1) + 31) / 32) * 32 * 32);  // Ldiag: L of every 32x32 diagonal block
   a->dx = c.take<float>(std::max(n, 1));
   a->info = c.take<int>(4);
   a->done = a->info + 1;

@@ -332,44 +332,8 @@ __device__ __forceinline__ void diag_step(double (&r)[PNB], int lane, bool& bad)
   }
 }
 
-// PNBxPNB diagonal block by one wave (lanes 0..31 = rows, in registers; static indices because the
-// steps are compile-time). Also writes L11^T to Lt for the panel solve (scalar-loadable there).
-__global__ void __launch_bounds__(64) chol_diag_kernel(double* __restrict__ H, double* __restrict__ Lt, int n, int k0,
-                                                       int* __restrict__ info, const int* __restrict__ done) {
-  if (*done) return;
-  const int kb = min(PNB, n - k0);
-  __shared__ double S[PNB][PNB + 1];
-  const int lane = threadIdx.x;
-  const int li = min(lane, PNB - 1);
-  {
-    double v[PNB];
-#pragma unroll
-    for (int t = 0; t < PNB; t++) v[t] = H[(size_t)(k0 + min(t, kb - 1)) * n + k0 + min(li, kb - 1)];
-    if (lane < PNB)
-#pragma unroll
-      for (int t = 0; t < PNB; t++) S[t][lane] = (t < kb && lane < kb && lane <= t) ? v[t] : 0.0;
-  }
-  wave_sync();
-  double r[PNB];
-#pragma unroll
-  for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
-  bool bad = false;
-  diag_step<0>(r, lane, bad);
-  if (bad && lane == 0) *info = 1;
-  wave_sync();
-  if (lane < PNB)
-#pragma unroll
-    for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
-  wave_sync();
-  if (lane < PNB) {
-    for (int t = 0; t < kb; t++)  // coalesced write-back of the lower triangle (lane = column)
-      if (lane <= t) H[(size_t)(k0 + t) * n + k0 + lane] = S[t][lane];
-    for (int t = 0; t < PNB; t++) Lt[t * PNB + lane] = S[lane][t];  // Lt[j][k] = L[k][j] (padded)
-  }
-}
-
 // Right-looking step J of the register-row forward substitution: x_J *= 1/L_JJ, then fold x_J into
-// the later columns with column J of L11 (= row J of Lt, staged in LDS: broadcast reads; no compiler
+// the later columns with column J of L11 (= row J of Ls = L11^T in LDS: broadcast reads; no compiler
 // barrier here — a memory clobber inside the unrolled steps makes the allocator spill x[]).
 template <int J>
 __device__ __forceinline__ void trsm_step(double (&x)[PNB], const double (*Ls)[PNB + 2]) {
@@ -384,34 +348,56 @@ __device__ __forceinline__ void trsm_step(double (&x)[PNB], const double (*Ls)[P
   }
 }
 
-// rows r in [k0+kb, n] (row n = rhs): L21 = A21 L11^-T. One wave per 64 rows, lane = row, its PNB
-// panel entries in registers; L11^T (from the diagonal kernel) staged in LDS with the pivots'
-// reciprocals.
-__global__ void __launch_bounds__(64) chol_trsm_kernel(double* __restrict__ H, const double* __restrict__ Lt, int n,
-                                                       int k0, const int* __restrict__ done) {
+// One panel: every block (one wave, 64 rows) factors the PNBxPNB diagonal block itself (lanes
+// 0..31 = rows in registers, readlane broadcasts) — redundant across blocks but it removes a launch
+// and a dependency from the critical path — then solves its rows r in [k0+kb, n] (row n = rhs):
+// L21 = A21 L11^-T. L11 goes to Ldiag[panel] (block 0), never back into H: other blocks may still
+// be reading A11 from H.
+__global__ void __launch_bounds__(64) chol_panel_kernel(double* __restrict__ H, double* __restrict__ Ldiag, int n,
+                                                        int k0, int* __restrict__ info, const int* __restrict__ done) {
   if (*done) return;
   const int kb = min(PNB, n - k0);
-  const int lane = threadIdx.x;
+  __shared__ double S[PNB][PNB + 1];
   __shared__ double Ls[PNB][PNB + 2];
+  const int lane = threadIdx.x;
+  const int li = min(lane, PNB - 1);
   {
-    double v[PNB * PNB / 64];
+    double v[PNB];
 #pragma unroll
-    for (int u = 0; u < PNB * PNB / 64; u++) v[u] = Lt[lane + 64 * u];
+    for (int t = 0; t < PNB; t++) v[t] = H[(size_t)(k0 + min(t, kb - 1)) * n + k0 + min(li, kb - 1)];
+    if (lane < PNB)
 #pragma unroll
-    for (int u = 0; u < PNB * PNB / 64; u++) {
-      const int t = lane + 64 * u;
-      Ls[t / PNB][t % PNB] = v[u];
+      for (int t = 0; t < PNB; t++) S[t][lane] = (t < kb && lane < kb && lane <= t) ? v[t] : 0.0;
+  }
+  wave_sync();
+  {
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
+    bool bad = false;
+    diag_step<0>(r, lane, bad);
+    if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
+    wave_sync();
+    if (lane < PNB)
+#pragma unroll
+      for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
+  }
+  wave_sync();
+  if (lane < PNB) {
+    for (int t = 0; t < PNB; t++) Ls[t][lane] = S[lane][t];  // Ls = L11^T (padded)
+    Ls[lane][PNB] = 1.0 / S[lane][lane];
+    if (blockIdx.x == 0) {
+      double* Ld = Ldiag + (size_t)(k0 / PNB) * PNB * PNB;
+      for (int t = 0; t < PNB; t++) Ld[t * PNB + lane] = S[t][lane];  // row-major L11 (padded)
     }
   }
   wave_sync();
-  if (lane < PNB) Ls[lane][PNB] = 1.0 / Ls[lane][lane];
   const int r = k0 + kb + blockIdx.x * 64 + lane;
   const int rr = min(r, n);
   double* row = H + (size_t)rr * n + k0;
   double x[PNB];
 #pragma unroll
   for (int c = 0; c < PNB; c++) x[c] = c < kb ? row[min(c, kb - 1)] : 0.0;
-  wave_sync();
   trsm_step<0>(x, Ls);
   if (r <= n) {
     // branch-free stores (a per-column `if (c < kb)` makes the allocator spill x[]): columns past
@@ -490,7 +476,8 @@ __global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H
 // panels from the end; per panel the solved tail is folded in by a 16-group x 64-column GEMV, then
 // wave 0 back-solves the 64x64 diagonal block with lane shuffles. x stays in LDS (n <= 8192).
 #define BK_NB 64
-__global__ void __launch_bounds__(1024) chol_back_all_kernel(const double* __restrict__ H, double* __restrict__ xg,
+__global__ void __launch_bounds__(1024) chol_back_all_kernel(const double* __restrict__ H,
+                                                             const double* __restrict__ Ldiag, double* __restrict__ xg,
                                                              int n, const int* __restrict__ done) {
   if (*done) return;
   __shared__ double xs[8192];
@@ -511,7 +498,14 @@ __global__ void __launch_bounds__(1024) chol_back_all_kernel(const double* __res
     part[g][c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     for (int t = threadIdx.x; t < BK_NB * BK_NB; t += 1024) {
       const int i = t / BK_NB, j = t % BK_NB;
-      Ld[i][j] = (i < kb && j <= i) ? H[(size_t)(k0 + i) * n + k0 + j] : 0.0;
+      double v = 0.0;
+      if (i < kb && j <= i) {
+        if (i / PNB == j / PNB)  // inside a PNB diagonal block: kept in Ldiag by the panel kernel
+          v = Ldiag[(size_t)((k0 + i) / PNB) * PNB * PNB + (i % PNB) * PNB + (j % PNB)];
+        else
+          v = H[(size_t)(k0 + i) * n + k0 + j];
+      }
+      Ld[i][j] = v;
     }
     __syncthreads();
     if (threadIdx.x < 64) {
@@ -589,17 +583,14 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
     hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows), dim3(64), 0, s, *a, n, nblocks);
     for (int k0 = 0; k0 < n; k0 += PNB) {
       const int kb = n - k0 < PNB ? n - k0 : PNB;
-      hipLaunchKernelGGL(m3s::chol_diag_kernel, dim3(1), dim3(64), 0, s, a->H, a->Lt, n, k0, a->info, a->done);
-      const int rows = n + 1 - (k0 + kb);
-      if (rows > 0) {
-        hipLaunchKernelGGL(m3s::chol_trsm_kernel, dim3((rows + 63) / 64), dim3(64), 0, s, a->H, a->Lt, n, k0,
-                           a->done);
-        const int tr = (rows + UT - 1) / UT;
-        const int tc = (n - (k0 + kb) + UT - 1) / UT;
-        if (tc > 0) hipLaunchKernelGGL(m3s::chol_update_kernel, dim3(tr, tc), dim3(256), 0, s, a->H, n, k0, a->done);
-      }
+      const int rows = n + 1 - (k0 + kb);  // >= 1: the rhs row
+      hipLaunchKernelGGL(m3s::chol_panel_kernel, dim3((rows + 63) / 64), dim3(64), 0, s, a->H, a->Lt, n, k0, a->info,
+                         a->done);
+      const int tr = (rows + UT - 1) / UT;
+      const int tc = (n - (k0 + kb) + UT - 1) / UT;
+      if (tc > 0) hipLaunchKernelGGL(m3s::chol_update_kernel, dim3(tr, tc), dim3(256), 0, s, a->H, n, k0, a->done);
     }
-    hipLaunchKernelGGL(m3s::chol_back_all_kernel, dim3(1), dim3(1024), 0, s, a->H, a->x, n, a->done);
+    hipLaunchKernelGGL(m3s::chol_back_all_kernel, dim3(1), dim3(1024), 0, s, a->H, a->Lt, a->x, n, a->done);
   }
   hipLaunchKernelGGL(m3s::ba_retr_kernel, dim3(1), dim3(256), 0, s, *a, K, n, delta_thresh);
   return hipGetLastError();

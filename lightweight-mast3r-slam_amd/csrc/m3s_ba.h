@@ -38,7 +38,7 @@ struct BaArgs {
   const int* rhs_ent;
   double* H;   // ((n+1), n), n = 7(K-1); row n = rhs
   double* x;   // (n)
-  double* Lt;  // (64*64) current panel's L11 transposed (written by chol_diag, read by chol_trsm)
+  double* Lt;  // (ceil(n/32), 32, 32) L of every diagonal block (chol_panel -> chol_back_all)
   float* dx;   // (n) output, reference return value
   int* info;   // factorisation failure flag
   int* done;   // early-exit flag (|dx| < delta_thresh)
