@@ -25,29 +25,34 @@ def match(X11, X21, D11, D21, idx_1_to_2_init=None):
     return match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init)
 
 
+def _f32(t):
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+
+
 def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None):
     cfg = config["matching"]
     lib = _lib.load()
     _lib.require_cuda("match", X11, X21, D11, D21, idx_1_to_2_init)
     b, h, w = X21.shape[:3]
     F = D11.shape[-1]
-    X11 = X11.float().contiguous()
-    X21 = X21.float().contiguous()
-    D11 = D11.float().contiguous()
-    D21 = D21.float().reshape(b, h, w, F).contiguous()
+    X11, X21, D11 = _f32(X11), _f32(X21), _f32(D11)
+    D21 = _f32(D21).reshape(b, h, w, F)
     if tuple(X11.shape) != (b, h, w, 3) or tuple(D11.shape) != (b, h, w, F):
         raise RuntimeError("match: X11/X21 (B,H,W,3) and D11/D21 (B,H,W,F) must agree")
-    init = None
+    init = 0
     if idx_1_to_2_init is not None:
-        init = idx_1_to_2_init.to(torch.int64).reshape(b, h * w).contiguous()
+        init_t = idx_1_to_2_init
+        if init_t.dtype != torch.int64 or not init_t.is_contiguous():
+            init_t = init_t.to(torch.int64).contiguous()
+        if init_t.numel() != b * h * w:
+            raise RuntimeError("match: idx_1_to_2_init must hold B*H*W indices")
+        init = init_t.data_ptr()
     dev = X11.device
     idx = torch.empty((b, h * w), dtype=torch.int64, device=dev)
     valid = torch.empty((b, h * w, 1), dtype=torch.bool, device=dev)
-    nbytes = lib.m3s_match_workspace_size(b, h, w, F)
-    ws = _lib.workspace("match", nbytes, dev)
-    _lib.check(lib.m3s_match(_lib.ptr(X11), _lib.ptr(X21), _lib.ptr(D11), _lib.ptr(D21), _lib.ptr(init),
-                             _lib.ptr(idx), _lib.ptr(valid), b, h, w, F, int(cfg["max_iter"]),
-                             float(cfg["lambda_init"]), float(cfg["convergence_thresh"]), float(cfg["dist_thresh"]),
-                             int(cfg["radius"]), int(cfg["dilation_max"]), _lib.ptr(ws), ws.numel(),
-                             _lib.stream_ptr(dev)))
+    ws = _lib.workspace("match", lib.m3s_match_workspace_size(b, h, w, F), dev)
+    _lib.check(lib.m3s_match(X11.data_ptr(), X21.data_ptr(), D11.data_ptr(), D21.data_ptr(), init, idx.data_ptr(),
+                             valid.data_ptr(), b, h, w, F, int(cfg["max_iter"]), float(cfg["lambda_init"]),
+                             float(cfg["convergence_thresh"]), float(cfg["dist_thresh"]), int(cfg["radius"]),
+                             int(cfg["dilation_max"]), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
     return idx, valid
