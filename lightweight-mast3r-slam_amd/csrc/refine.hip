@@ -7,10 +7,10 @@
 // after each level.
 //
 // MI355X design: one 32x8 pixel tile per 256-lane block (4 blocks / CU, 40 KiB LDS each).
-//   * Per level the block estimates the tile's flow (mean centre displacement), takes the bbox of
-//     the centres within 16 px of it, places a 64-column x 40-row window over bbox +- 3d and streams
-//     D11 (f16) into LDS in three 8-channel chunks (16 B / px) with global_load_lds — one
-//     wave-instruction per window row. Four resident blocks per CU hide each other's fill latency
+//   * Once per tile the block estimates the tile's flow (mean initial centre displacement); per level
+//     it takes the bbox of the centres within 16 px of it, places a 64-column x 40-row window over
+//     bbox +- 3d and streams D11 (f16) into LDS in three 8-channel chunks (16 B / px) with
+//     global_load_lds — one wave-instruction per window row. Four resident blocks per CU hide each other's fill latency
 //     (measured: faster than double-buffering at two blocks per CU).
 //   * Levels are specialised on d, so every candidate read is one ds_read_b128 with an immediate
 //     offset from a single per-lane base; the 49 running half sums live in registers across the
@@ -86,6 +86,7 @@ __device__ __forceinline__ void score_chunk(const uint4* base, const h2* q4, h1*
 struct TileCtx {
   const h1* img;
   int H, W, lane, wid, u_pix, v_pix;
+  int fu, fv;   // tile flow estimate: mean initial centre displacement (fixed for all levels)
   int bn;       // batch * N + pixel
   int4* olist;  // deferred-pixel list (nullable: score outliers in place)
   int* ocount;
@@ -96,26 +97,8 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
                                              h1& max_score, uint4* lds, int (*s_red)[4]) {
   constexpr int R = 3, G = 2 * R + 1, F = 24, RD = R * D;
   const int lane = t.lane, wid = t.wid, H = t.H, W = t.W;
-  // 1) tile flow estimate: mean centre displacement (cu - u_pix) over active lanes
-  int su = active ? cu - t.u_pix : 0, sv = active ? cv - t.v_pix : 0, na = active ? 1 : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    su += __shfl_xor(su, off, 64);
-    sv += __shfl_xor(sv, off, 64);
-    na += __shfl_xor(na, off, 64);
-  }
-  __syncthreads();  // previous level's readers of s_red / lds are done
-  if (lane == 0) {
-    s_red[wid][0] = su;
-    s_red[wid][1] = sv;
-    s_red[wid][2] = na;
-  }
-  __syncthreads();
-  const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
-  const int fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
-  const int fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
-  // 2) bbox of the inlier centres (within 16 px of pixel + tile flow)
-  const bool inl = active && abs(cu - t.u_pix - fu) <= 16 && abs(cv - t.v_pix - fv) <= 16;
+  // bbox of the inlier centres (within 16 px of pixel + the tile's flow estimate t.fu/t.fv)
+  const bool inl = active && abs(cu - t.u_pix - t.fu) <= 16 && abs(cv - t.v_pix - t.fv) <= 16;
   int mnu = inl ? cu : INT_MAX, mxu = inl ? cu : INT_MIN;
   int mnv = inl ? cv : INT_MAX, mxv = inl ? cv : INT_MIN;
 #pragma unroll
@@ -125,7 +108,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     mnv = min(mnv, __shfl_xor(mnv, off, 64));
     mxv = max(mxv, __shfl_xor(mxv, off, 64));
   }
-  __syncthreads();
+  __syncthreads();  // previous level's readers of s_red / lds are done
   if (lane == 0) {
     s_red[wid][0] = mnu;
     s_red[wid][1] = mxu;
@@ -200,35 +183,46 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #pragma unroll
   for (int c = 0; c < G * G; c++) s[c] = (h1)0.0f;
   __syncthreads();  // the reduction scratch aliases the window: its readers are done
+  const int lane_off = gx * F;  // per-lane column offset; the row base is wave-uniform (scalar)
 #pragma unroll
   for (int chunk = 0; chunk < F / 8; chunk++) {
     if (chunk) __syncthreads();  // previous chunk's readers are done
     for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
-      __builtin_amdgcn_global_load_lds((gvoid_t)(t.img + ((size_t)gy * W + gx) * F + chunk * 8),
-                                       (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+      const h1* rowp = t.img + (size_t)gy * W * F + chunk * 8;
+      __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (lane_in) score_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], s);
   }
   if (lane_in) {  // scan-order arg-max: u outer, v inner, strict '>' (matching_kernels.cu:54-71)
-    int bu = cu, bvv = cv;
+    int bi = -1;
+    if (__ballot(lane_in && !(u_lo >= 0 && u_lo + 6 * D < W && v_lo >= 0 && v_lo + 6 * D < H)) == 0) {
+      // every candidate grid of the wave lies inside the image: index-only tracking
 #pragma unroll
-    for (int i = 0; i < G; i++) {
-      const bool uok = u_lo + i * D >= 0 && u_lo + i * D < W;
+      for (int c = 0; c < G * G; c++) {
+        const bool gt = s[c] > max_score;
+        max_score = gt ? s[c] : max_score;
+        bi = gt ? c : bi;
+      }
+    } else {
 #pragma unroll
-      for (int j = 0; j < G; j++) {
-        const bool vok = v_lo + j * D >= 0 && v_lo + j * D < H;
-        if (uok && vok && s[i * G + j] > max_score) {
-          max_score = s[i * G + j];
-          bu = u_lo + i * D;
-          bvv = v_lo + j * D;
+      for (int i = 0; i < G; i++) {
+        const bool uok = u_lo + i * D >= 0 && u_lo + i * D < W;
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+          const bool vok = v_lo + j * D >= 0 && v_lo + j * D < H;
+          const bool gt = uok && vok && s[i * G + j] > max_score;
+          max_score = gt ? s[i * G + j] : max_score;
+          bi = gt ? i * G + j : bi;
         }
       }
     }
-    cu = bu;
-    cv = bvv;
+    if (bi >= 0) {
+      cu = u_lo + (bi / G) * D;
+      cv = v_lo + (bi % G) * D;
+    }
   }
 }
 
@@ -288,6 +282,25 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
   } else {
 #pragma unroll
     for (int k = 0; k < F / 2; k++) q[k] = h2{(h1)0.0f, (h1)0.0f};
+  }
+  {  // tile flow estimate, once per tile: the centres move by at most 3d per level, well inside the
+     // +-16 px inlier band, so the initial mean serves every level (saves a block reduction per level)
+    int su = active ? cu - t.u_pix : 0, sv = active ? cv - t.v_pix : 0, na = active ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      su += __shfl_xor(su, off, 64);
+      sv += __shfl_xor(sv, off, 64);
+      na += __shfl_xor(na, off, 64);
+    }
+    if (t.lane == 0) {
+      s_red[t.wid][0] = su;
+      s_red[t.wid][1] = sv;
+      s_red[t.wid][2] = na;
+    }
+    __syncthreads();
+    const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
+    t.fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
+    t.fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
   }
   const bool mine = active;  // deferred pixels are written by refine_outlier_kernel
   h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
