@@ -287,10 +287,11 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 }
 
 // ------------------------------------------------------------------------------------------
-// dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1.
-// Panels of PNB = 32 columns: the serial work per panel (diagonal factorisation, one wave) grows
-// with PNB^2 per lane, so a narrow panel keeps the critical path short; the trailing update runs
-// on 64x64 tiles of depth PNB.
+// dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1, right-looking with a
+// one-panel look-ahead: launch s factors panel s (PNB = 32 columns) while panel s-1's trailing
+// update of the columns beyond panel s runs beside it in the same grid. The panel blocks apply
+// panel s-1's update to their own column block first, so the update of the rest of the matrix is
+// off the critical path (one launch per panel instead of a panel launch + an update launch).
 // ------------------------------------------------------------------------------------------
 #define PNB 32
 #define UT 64
@@ -309,6 +310,16 @@ __device__ __forceinline__ double bcast_lane(double v, int src) {
   return *reinterpret_cast<double*>(&x);
 }
 
+// 1/sqrt(d) for d > 0 to ~1 ulp: v_rsq_f64 estimate refined by two Newton steps — a fraction of the
+// latency of the correctly rounded sqrt + divide sequences on the pivot chain.
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+#pragma unroll
+  for (int it = 0; it < 2; it++) y = fma(y, fma(-h * y, y, 0.5), y);
+  return y;
+}
+
 // Right-looking column step J of the register-row diagonal factorisation: pivot and column
 // multipliers broadcast with readlane, rank-1 update of the lane's own row. Rows/columns >= kb are
 // padded with the identity, so every step is valid and the padding stays inert.
@@ -320,8 +331,8 @@ __device__ __forceinline__ void diag_step(double (&r)[PNB], int lane, bool& bad)
       bad = true;
       d = 1.0;
     }
-    const double sj = sqrt(d);
-    const double inv = 1.0 / sj;
+    const double inv = rsqrt_nr(d);  // 1/sqrt(d): hardware estimate + two Newton steps (serial chain)
+    const double sj = d * inv;
     // unconditional multiplier (a lane-dependent select here makes the allocator spill r[]); lanes
     // <= J only disturb their own strictly-upper entries, which are never read
     const double l = r[J] * inv;
@@ -333,200 +344,321 @@ __device__ __forceinline__ void diag_step(double (&r)[PNB], int lane, bool& bad)
 }
 
 // Right-looking step J of the register-row forward substitution: x_J *= 1/L_JJ, then fold x_J into
-// the later columns with column J of L11 (= row J of Ls = L11^T in LDS: broadcast reads; no compiler
-// barrier here — a memory clobber inside the unrolled steps makes the allocator spill x[]).
+// the later columns with column J of L11 (row J of Ls = L11^T in LDS). Row J+1 is read from LDS
+// before step J's FMAs (software pipelining: the broadcast reads' latency hides behind them).
 template <int J>
-__device__ __forceinline__ void trsm_step(double (&x)[PNB], const double (*Ls)[PNB + 2]) {
+__device__ __forceinline__ void trsm_pipe(double (&x)[PNB], const double (*Ls)[PNB + 2], const double (&cur)[PNB + 2]) {
   if constexpr (J < PNB) {
-    x[J] *= Ls[J][PNB];  // reciprocal of the pivot, stored after the row
+    double nxt[PNB + 2];
+    if constexpr (J + 1 < PNB) {
 #pragma unroll
-    for (int k0 = J + 1; k0 < PNB; k0 += 8) {
-#pragma unroll
-      for (int k = k0; k < (k0 + 8 < PNB ? k0 + 8 : PNB); k++) x[k] -= x[J] * Ls[J][k];
+      for (int c = (J + 2) & ~1; c < PNB + 2; c += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(&Ls[J + 1][c]);
+        nxt[c] = v.x;
+        nxt[c + 1] = v.y;
+      }
     }
-    trsm_step<J + 1>(x, Ls);
+    x[J] *= cur[PNB];  // reciprocal of the pivot, stored after the row
+#pragma unroll
+    for (int k = J + 1; k < PNB; k++) x[k] -= x[J] * cur[k];
+    trsm_pipe<J + 1>(x, Ls, nxt);
   }
 }
 
-// One panel: every block (one wave, 64 rows) factors the PNBxPNB diagonal block itself (lanes
-// 0..31 = rows in registers, readlane broadcasts) — redundant across blocks but it removes a launch
-// and a dependency from the critical path — then solves its rows r in [k0+kb, n] (row n = rhs):
-// L21 = A21 L11^-T. L11 goes to Ldiag[panel] (block 0), never back into H: other blocks may still
-// be reading A11 from H.
-__global__ void __launch_bounds__(64) chol_panel_kernel(double* __restrict__ H, double* __restrict__ Ldiag, int n,
-                                                        int k0, int* __restrict__ info, const int* __restrict__ done) {
+// Launch s of the factorisation (k0 = s*PNB, kb = panel width). Blocks [0, P): 64 rows each of
+// panel s below its diagonal block (row n = rhs included):
+//   1. coalesced loads of A11 (diagonal block), the block's rows A21 and, for s > 0, the matching
+//      rows of panel s-1 (L_{s,s-1} and L_{R,s-1});
+//   2. s > 0: A11 -= L_{s,s-1} L_{s,s-1}^T, A21 -= L_{R,s-1} L_{s,s-1}^T (the look-ahead update);
+//   3. wave 0 factors A11 (every block redundantly: no extra launch or dependency on the critical
+//      path; lanes = rows in registers, readlane broadcasts), block 0 keeps L11 in Ldiag;
+//   4. wave 0 solves L21 = A21 L11^-T (lane = row) and the block stores it coalesced.
+// Blocks [P, P+U): panel s-1's update A22 -= L21 L21^T over the UTxUT lower tiles of the columns
+// beyond panel s (rows and columns from k0+kb; the lower-triangle tiles enumerated, none idle).
+// L11 never goes back into H; later launches read the diagonal blocks from Ldiag.
+__global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, double* __restrict__ Ldiag, int n,
+                                                        int k0, int P, int* __restrict__ info,
+                                                        const int* __restrict__ done) {
   if (*done) return;
+  constexpr int LD = PNB + 1;
+  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + 32 * (PNB + 2)];
   const int kb = min(PNB, n - k0);
-  __shared__ double S[PNB][PNB + 1];
-  __shared__ double Ls[PNB][PNB + 2];
-  const int lane = threadIdx.x;
-  const int li = min(lane, PNB - 1);
-  {
-    double v[PNB];
-#pragma unroll
-    for (int t = 0; t < PNB; t++) v[t] = H[(size_t)(k0 + min(t, kb - 1)) * n + k0 + min(li, kb - 1)];
-    if (lane < PNB)
-#pragma unroll
-      for (int t = 0; t < PNB; t++) S[t][lane] = (t < kb && lane < kb && lane <= t) ? v[t] : 0.0;
-  }
-  wave_sync();
-  {
-    double r[PNB];
-#pragma unroll
-    for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
-    bool bad = false;
-    diag_step<0>(r, lane, bad);
-    if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
-    wave_sync();
-    if (lane < PNB)
-#pragma unroll
-      for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
-  }
-  wave_sync();
-  if (lane < PNB) {
-    for (int t = 0; t < PNB; t++) Ls[t][lane] = S[lane][t];  // Ls = L11^T (padded)
-    Ls[lane][PNB] = 1.0 / S[lane][lane];
-    if (blockIdx.x == 0) {
-      double* Ld = Ldiag + (size_t)(k0 / PNB) * PNB * PNB;
-      for (int t = 0; t < PNB; t++) Ld[t * PNB + lane] = S[t][lane];  // row-major L11 (padded)
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x >= P) {
+    // ---- trailing update of panel s-1 (columns PNB wide at kp) beyond panel s ----
+    const int kp = k0 - PNB, st = k0 + kb;
+    const int T = (n - st + UT - 1) / UT;  // column tiles
+    const int tri = T * (T + 1) / 2;
+    const int u = blockIdx.x - P;
+    int ti, tj;
+    if (u < tri) {
+      ti = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+      while (ti * (ti + 1) / 2 > u) ti--;
+      while ((ti + 1) * (ti + 2) / 2 <= u) ti++;
+      tj = u - ti * (ti + 1) / 2;
+    } else {  // the extra tile row holding only the rhs row (when n - st is a multiple of UT)
+      ti = T;
+      tj = u - tri;
     }
-  }
-  wave_sync();
-  const int r = k0 + kb + blockIdx.x * 64 + lane;
-  const int rr = min(r, n);
-  double* row = H + (size_t)rr * n + k0;
-  double x[PNB];
+    const int r0 = st + ti * UT, c0 = st + tj * UT;
+    const int nr = min(UT, n + 1 - r0), nc = min(UT, n - c0);
+    double(*A)[LD] = reinterpret_cast<double(*)[LD]>(smem);
+    double(*B)[LD] = reinterpret_cast<double(*)[LD]>(smem + 64 * LD);
+    const int ty = t / 16, tx = t % 16;  // 4x4 outputs per lane
+    {  // 8 + 8 panel loads and the 16 output-tile loads per lane, all issued before any use
+      double av[8], bv[8];
 #pragma unroll
-  for (int c = 0; c < PNB; c++) x[c] = c < kb ? row[min(c, kb - 1)] : 0.0;
-  trsm_step<0>(x, Ls);
-  if (r <= n) {
-    // branch-free stores (a per-column `if (c < kb)` makes the allocator spill x[]): columns past
-    // kb rewrite column kb-1 with its own value
-    double keep = x[0];  // x[kb - 1], selected without dynamic indexing
+      for (int q = 0; q < 8; q++) {
+        const int e = t + 256 * q, i = e / PNB, k = e % PNB;
+        av[q] = H[(size_t)(r0 + min(i, nr - 1)) * n + kp + k];
+        bv[q] = H[(size_t)(c0 + min(i, nc - 1)) * n + kp + k];
+      }
 #pragma unroll
-    for (int c = 1; c < PNB; c++) keep = (c == kb - 1) ? x[c] : keep;
-#pragma unroll
-    for (int c = 0; c < PNB; c++) row[min(c, kb - 1)] = c < kb ? x[c] : keep;
-  }
-}
-
-// trailing update A22 -= L21 L21^T over UTxUT lower tiles, depth kb <= PNB; rows [s, n], cols [s, n-1]
-__global__ void __launch_bounds__(256) chol_update_kernel(double* __restrict__ H, int n, int k0,
-                                                          const int* __restrict__ done) {
-  if (*done) return;
-  const int kb = min(PNB, n - k0);
-  const int s = k0 + kb;
-  const int ti = blockIdx.x, tj = blockIdx.y;
-  if (tj > ti) return;
-  const int r0 = s + ti * UT, c0 = s + tj * UT;
-  if (c0 >= n) return;
-  const int nr = min(UT, n + 1 - r0), nc = min(UT, n - c0);
-  __shared__ double A[UT][PNB + 1];
-  __shared__ double B[UT][PNB + 1];
-  {  // 8 + 8 per lane, branch-free, all loads issued before the LDS stores
-    double av[8], bv[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / PNB, k = t % PNB;
-      const int kc = min(k, kb - 1);
-      av[u] = H[(size_t)(r0 + min(i, nr - 1)) * n + k0 + kc];
-      bv[u] = H[(size_t)(c0 + min(i, nc - 1)) * n + k0 + kc];
+      for (int q = 0; q < 8; q++) {
+        const int e = t + 256 * q, i = e / PNB, k = e % PNB;
+        A[i][k] = i < nr ? av[q] : 0.0;
+        B[i][k] = i < nc ? bv[q] : 0.0;
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int t = threadIdx.x + 256 * u, i = t / PNB, k = t % PNB;
-      A[i][k] = (i < nr && k < kb) ? av[u] : 0.0;
-      B[i][k] = (i < nc && k < kb) ? bv[u] : 0.0;
-    }
-  }
-  __syncthreads();
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;  // 4x4 outputs per lane
-  double acc[4][4];
-#pragma unroll
-  for (int x = 0; x < 4; x++)
-#pragma unroll
-    for (int y = 0; y < 4; y++) acc[x][y] = 0.0;
-#pragma unroll 8
-  for (int k = 0; k < PNB; k++) {
-    double av[4], bv[4];
-#pragma unroll
-    for (int x = 0; x < 4; x++) av[x] = A[ty + 16 * x][k];
-#pragma unroll
-    for (int y = 0; y < 4; y++) bv[y] = B[tx + 16 * y][k];
+    double cold[4][4];
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
-      for (int y = 0; y < 4; y++) acc[x][y] += av[x] * bv[y];
-  }
+      for (int y = 0; y < 4; y++)
+        cold[x][y] = H[(size_t)(r0 + min(ty + 16 * x, nr - 1)) * n + c0 + min(tx + 16 * y, nc - 1)];
+    __syncthreads();
+    double acc[4][4];
 #pragma unroll
-  for (int x = 0; x < 4; x++) {
-    const int i = ty + 16 * x;
-    if (i >= nr) continue;
+    for (int x = 0; x < 4; x++)
 #pragma unroll
-    for (int y = 0; y < 4; y++) {
-      const int j = tx + 16 * y;
-      if (j >= nc) continue;
-      if (r0 + i < n && c0 + j > r0 + i) continue;  // strictly-upper part unused
-      H[(size_t)(r0 + i) * n + c0 + j] -= acc[x][y];
+      for (int y = 0; y < 4; y++) acc[x][y] = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < PNB; k++) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int x = 0; x < 4; x++) av[x] = A[ty + 16 * x][k];
+#pragma unroll
+      for (int y = 0; y < 4; y++) bv[y] = B[tx + 16 * y][k];
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] += av[x] * bv[y];
     }
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      const int i = ty + 16 * x;
+      if (i >= nr) continue;
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        const int j = tx + 16 * y;
+        if (j >= nc) continue;
+        if (r0 + i < n && c0 + j > r0 + i) continue;  // strictly-upper part unused
+        H[(size_t)(r0 + i) * n + c0 + j] = cold[x][y] - acc[x][y];
+      }
+    }
+    return;
+  }
+  // ---- panel s ----
+  double(*S)[LD] = reinterpret_cast<double(*)[LD]>(smem);             // A11 -> L11
+  double(*P1)[LD] = reinterpret_cast<double(*)[LD]>(smem + 32 * LD);  // L_{s,s-1}
+  double(*X)[LD] = reinterpret_cast<double(*)[LD]>(smem + 64 * LD);   // A21 -> L21 (64 rows)
+  double(*LR)[LD] = reinterpret_cast<double(*)[LD]>(smem + 128 * LD); // L_{R,s-1}
+  double(*Ls)[PNB + 2] = reinterpret_cast<double(*)[PNB + 2]>(smem + 192 * LD);
+  const bool upd = k0 > 0;
+  const int kp = k0 - PNB;
+  const int rbase = k0 + kb + blockIdx.x * 64;
+  const int col = t & 31, rs = t >> 5;  // loads: column col of rows rs + 8q
+  {
+    const int cc = min(col, kb - 1);
+    double sv[4], pv[4], xv[8], lv[8];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int rr = k0 + min(rs + 8 * q, kb - 1);
+      sv[q] = H[(size_t)rr * n + k0 + cc];
+      if (upd) pv[q] = H[(size_t)rr * n + kp + col];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int rr = min(rbase + rs + 8 * q, n);
+      xv[q] = H[(size_t)rr * n + k0 + cc];
+      if (upd) lv[q] = H[(size_t)rr * n + kp + col];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int i = rs + 8 * q;
+      S[i][col] = (i < kb && col < kb && col <= i) ? sv[q] : 0.0;
+      P1[i][col] = (upd && i < kb) ? pv[q] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int i = rs + 8 * q;
+      X[i][col] = col < kb ? xv[q] : 0.0;
+      LR[i][col] = upd ? lv[q] : 0.0;
+    }
+  }
+  __syncthreads();
+  if (upd) {  // look-ahead update of this column block by panel s-1
+    {         // A21 rows: thread -> row t/4, columns 8*(t%4) .. +7
+      const int i = t >> 2, j0 = (t & 3) * 8;
+      double acc[8];
+#pragma unroll
+      for (int m = 0; m < 8; m++) acc[m] = 0.0;
+#pragma unroll 8
+      for (int k = 0; k < PNB; k++) {
+        const double a = LR[i][k];
+#pragma unroll
+        for (int m = 0; m < 8; m++) acc[m] += a * P1[j0 + m][k];
+      }
+#pragma unroll
+      for (int m = 0; m < 8; m++) X[i][j0 + m] -= (j0 + m < kb) ? acc[m] : 0.0;
+    }
+    {  // A11: thread -> row t/8, columns 4*(t%8) .. +3 (lower part kept)
+      const int i = t >> 3, j0 = (t & 7) * 4;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 8
+      for (int k = 0; k < PNB; k++) {
+        const double a = P1[i][k];
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[m] += a * P1[j0 + m][k];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+        if (j0 + m <= i) S[i][j0 + m] -= acc[m];
+    }
+    __syncthreads();
+  }
+  if (t < 64) {
+    const int lane = t, li = min(lane, PNB - 1);
+    {
+      double r[PNB];
+#pragma unroll
+      for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
+      bool bad = false;
+      diag_step<0>(r, lane, bad);
+      if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
+      wave_sync();
+      if (lane < PNB)
+#pragma unroll
+        for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
+    }
+    wave_sync();
+    if (lane < PNB) {
+      for (int q = 0; q < PNB; q++) Ls[q][lane] = S[lane][q];  // Ls = L11^T (padded)
+      const double dj = S[lane][lane];
+      double y = __builtin_amdgcn_rcp(dj);  // 1/L_jj: estimate + two Newton steps
+      y = fma(y, fma(-dj, y, 1.0), y);
+      y = fma(y, fma(-dj, y, 1.0), y);
+      Ls[lane][PNB] = y;
+      Ls[lane][PNB + 1] = 0.0;
+      if (blockIdx.x == 0) {
+        double* Ld = Ldiag + (size_t)(k0 / PNB) * PNB * PNB;
+        for (int q = 0; q < PNB; q++) Ld[q * PNB + lane] = S[q][lane];  // row-major L11 (padded)
+      }
+    }
+    wave_sync();
+    double x[PNB], row0[PNB + 2];
+#pragma unroll
+    for (int c = 0; c < PNB; c++) x[c] = X[lane][c];
+#pragma unroll
+    for (int c = 0; c < PNB + 2; c += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(&Ls[0][c]);
+      row0[c] = v.x;
+      row0[c + 1] = v.y;
+    }
+    trsm_pipe<0>(x, Ls, row0);
+#pragma unroll
+    for (int c = 0; c < PNB; c++) X[lane][c] = x[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int i = rs + 8 * q, rw = rbase + i;
+    if (rw <= n && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
   }
 }
 
-// Whole back substitution L^T x = y (y = row n after the factorisation) in ONE block: 64-column
-// panels from the end; per panel the solved tail is folded in by a 16-group x 64-column GEMV, then
-// wave 0 back-solves the 64x64 diagonal block with lane shuffles. x stays in LDS (n <= 8192).
-#define BK_NB 64
-__global__ void __launch_bounds__(1024) chol_back_all_kernel(const double* __restrict__ H,
-                                                             const double* __restrict__ Ldiag, double* __restrict__ xg,
-                                                             int n, const int* __restrict__ done) {
+// Back substitution L^T x = y (y = row n after the factorisation), one launch per BS_NB-column
+// panel from the end (right-looking):
+//   A (every block, redundantly): load the panel's diagonal block of L into LDS (its PNB-diagonal
+//     blocks from Ldiag) and back-solve it with one wave (lanes hold two unknowns each; x_c broadcast
+//     by readlane, the next row of L prefetched from LDS);
+//   B (block b, columns [b*BS_NB, (b+1)*BS_NB) below k0): y_j -= sum_r L[k0+r][j] x_r, read row-wise
+//     (coalesced) by two half-blocks, written back into row n for the next launch.
+// Replaces a single-block solve that streamed all of L through one CU.
+#define BS_NB 128
+__global__ void __launch_bounds__(1024) chol_back_step_kernel(double* __restrict__ H, const double* __restrict__ Ldiag,
+                                                              double* __restrict__ xg, int n, int k0,
+                                                              const int* __restrict__ done) {
   if (*done) return;
-  __shared__ double xs[8192];
-  __shared__ double part[16][BK_NB];
-  __shared__ double Ld[BK_NB][BK_NB + 1];
-  const int c = threadIdx.x % BK_NB, g = threadIdx.x / BK_NB;
-  for (int k0 = ((n - 1) / BK_NB) * BK_NB; k0 >= 0; k0 -= BK_NB) {
-    const int kb = min(BK_NB, n - k0);
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (c < kb) {
-      int r = k0 + kb + g;
-      for (; r + 48 < n; r += 64) {
+  const int kb = min(BS_NB, n - k0);
+  __shared__ double Ld[BS_NB][BS_NB + 1];
+  __shared__ double rd[BS_NB];
+  __shared__ double xs[BS_NB];
+  __shared__ double part[8][BS_NB];
+  const int t = threadIdx.x;
+  const double* yrow = H + (size_t)n * n;
+  // every global load of the launch is issued up front: the diagonal block (16 per thread) and the
+  // panel rows phase B multiplies (16 per thread; they do not depend on x)
+  double v[16], pb[16];
 #pragma unroll
-        for (int u = 0; u < 4; u++) acc[u] += H[(size_t)(r + 16 * u) * n + k0 + c] * xs[r + 16 * u];
-      }
-      for (; r < n; r += 16) acc[0] += H[(size_t)r * n + k0 + c] * xs[r];
-    }
-    part[g][c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    for (int t = threadIdx.x; t < BK_NB * BK_NB; t += 1024) {
-      const int i = t / BK_NB, j = t % BK_NB;
-      double v = 0.0;
-      if (i < kb && j <= i) {
-        if (i / PNB == j / PNB)  // inside a PNB diagonal block: kept in Ldiag by the panel kernel
-          v = Ldiag[(size_t)((k0 + i) / PNB) * PNB * PNB + (i % PNB) * PNB + (j % PNB)];
-        else
-          v = H[(size_t)(k0 + i) * n + k0 + j];
-      }
-      Ld[i][j] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      double y = 0.0;
-      if (lane < kb) {
-        double sp = 0.0;
-#pragma unroll
-        for (int q = 0; q < 16; q++) sp += part[q][lane];
-        y = H[(size_t)n * n + k0 + lane] - sp;
-      }
-      for (int cc = kb - 1; cc >= 0; cc--) {
-        const double xc = __shfl(y, cc, 64) / Ld[cc][cc];
-        if (lane == cc) y = xc;
-        if (lane < cc) y -= Ld[cc][lane] * xc;
-      }
-      if (lane < kb) xs[k0 + lane] = y;
-    }
-    __syncthreads();
+  for (int u = 0; u < 16; u++) {
+    const int e = u * 1024 + t, i = e / BS_NB, j = e % BS_NB;
+    const int ic = min(i, kb - 1), jc = min(j, ic);
+    v[u] = (ic / PNB == jc / PNB) ? Ldiag[(size_t)((k0 + ic) / PNB) * PNB * PNB + (ic % PNB) * PNB + (jc % PNB)]
+                                  : H[(size_t)(k0 + ic) * n + k0 + jc];
   }
-  for (int i = threadIdx.x; i < n; i += 1024) xg[i] = xs[i];
+  const int jl = t & (BS_NB - 1), rg = t >> 7;  // phase B: column jl, rows rg + 8u
+  const int j = blockIdx.x * BS_NB + jl;
+  if (k0 > 0) {
+    const int jc = min(j, k0 - 1);
+#pragma unroll
+    for (int u = 0; u < 16; u++) pb[u] = H[(size_t)(k0 + min(rg + 8 * u, kb - 1)) * n + jc];
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) {  // rows/columns past kb padded with the identity
+    const int e = u * 1024 + t, i = e / BS_NB, jj = e % BS_NB;
+    Ld[i][jj] = (i < kb && jj <= i) ? v[u] : (i == jj ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  if (t < BS_NB) {
+    const double d = Ld[t][t];
+    double y = __builtin_amdgcn_rcp(d);  // 1/L_cc: estimate + two Newton steps
+    y = fma(y, fma(-d, y, 1.0), y);
+    rd[t] = fma(y, fma(-d, y, 1.0), y);
+  }
+  __syncthreads();
+  if (t < 64) {  // one wave, two unknowns per lane, fully unrolled over the padded 128 columns
+    double y0 = t < kb ? yrow[k0 + t] : 0.0, y1 = t + 64 < kb ? yrow[k0 + t + 64] : 0.0;
+    // L[c][k] = 0 for k > c; k == c only disturbs the finished unknown c
+#pragma unroll 8
+    for (int c = BS_NB - 1; c >= 64; c--) {
+      const double xc = bcast_lane(y1, c - 64) * rd[c];
+      y0 -= Ld[c][t] * xc;
+      y1 -= Ld[c][t + 64] * xc;
+      if (t == 0) xs[c] = xc;
+    }
+#pragma unroll 8
+    for (int c = 63; c >= 0; c--) {
+      const double xc = bcast_lane(y0, c) * rd[c];
+      y0 -= Ld[c][t] * xc;
+      if (t == 0) xs[c] = xc;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && t < kb) xg[k0 + t] = xs[t];
+  if (k0 > 0) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < 16; u++) acc[u & 3] += pb[u] * xs[rg + 8 * u];  // xs = 0 past kb
+    part[rg][jl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (t < BS_NB && j < k0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int g = 0; g < 8; g++) sum += part[g][t];
+      H[(size_t)n * n + j] -= sum;
+    }
+  }
 }
 
 // dx = -x (or 0 when the factorisation failed), poses k >= 1 retracted, |dx| early exit.
@@ -583,14 +715,19 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
     hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows), dim3(64), 0, s, *a, n, nblocks);
     for (int k0 = 0; k0 < n; k0 += PNB) {
       const int kb = n - k0 < PNB ? n - k0 : PNB;
-      const int rows = n + 1 - (k0 + kb);  // >= 1: the rhs row
-      hipLaunchKernelGGL(m3s::chol_panel_kernel, dim3((rows + 63) / 64), dim3(64), 0, s, a->H, a->Lt, n, k0, a->info,
+      const int st = k0 + kb;
+      const int P = (n + 1 - st + 63) / 64;  // >= 1: the rhs row
+      int U = 0;
+      if (k0 > 0 && st < n) {
+        const int T = (n - st + UT - 1) / UT, R = (n + 1 - st + UT - 1) / UT;
+        U = T * (T + 1) / 2 + (R > T ? T : 0);
+      }
+      hipLaunchKernelGGL(m3s::chol_step_kernel, dim3(P + U), dim3(256), 0, s, a->H, a->Lt, n, k0, P, a->info,
                          a->done);
-      const int tr = (rows + UT - 1) / UT;
-      const int tc = (n - (k0 + kb) + UT - 1) / UT;
-      if (tc > 0) hipLaunchKernelGGL(m3s::chol_update_kernel, dim3(tr, tc), dim3(256), 0, s, a->H, n, k0, a->done);
     }
-    hipLaunchKernelGGL(m3s::chol_back_all_kernel, dim3(1), dim3(1024), 0, s, a->H, a->Lt, a->x, n, a->done);
+    for (int k0 = ((n - 1) / BS_NB) * BS_NB; k0 >= 0; k0 -= BS_NB)
+      hipLaunchKernelGGL(m3s::chol_back_step_kernel, dim3(k0 > 0 ? (k0 + BS_NB - 1) / BS_NB : 1), dim3(1024), 0, s,
+                         a->H, a->Lt, a->x, n, k0, a->done);
   }
   hipLaunchKernelGGL(m3s::ba_retr_kernel, dim3(1), dim3(256), 0, s, *a, K, n, delta_thresh);
   return hipGetLastError();

@@ -187,14 +187,18 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #pragma unroll
   for (int chunk = 0; chunk < F / 8; chunk++) {
     if (chunk) __syncthreads();  // previous chunk's readers are done
+#ifndef RT_NOLOAD
     for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
       const h1* rowp = t.img + (size_t)gy * W * F + chunk * 8;
       __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#ifndef RT_NOCOMP
     if (lane_in) score_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], s);
+#endif
   }
   if (lane_in) {  // scan-order arg-max: u outer, v inner, strict '>' (matching_kernels.cu:54-71)
     int bi = -1;

@@ -51,3 +51,16 @@ for rep in range(2):
     gb = E * H * W * 45 / 1e6  # MB -> MB/ms = GB/s
     print(f"rep {rep}: E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
           f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}", flush=True)
+
+if hasattr(lib, "m3s_debug_chol_stamps"):
+    buf = (ctypes.c_ulonglong * 512)()
+    lib.m3s_debug_chol_stamps(buf)
+    npan = min(64, (K - 1) * 7 // 32 + 1)
+    names = ["diag loaded", "diag factored", "Ls ready", "trsm done", "stored"]
+    acc = [0.0] * 5
+    for pnl in range(npan):
+        t0 = buf[pnl * 8]
+        for k in range(5):
+            acc[k] += (buf[pnl * 8 + k + 1] - t0) / 100.0
+    print("panel kernel block 0, mean over panels (us from start): " +
+          "  ".join(f"{n}={a / npan:.2f}" for n, a in zip(names, acc)))
