@@ -296,6 +296,8 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 #define PNB 32
 #define UT 64
 
+typedef double d4v __attribute__((ext_vector_type(4)));
+
 // lanes of one wave exchanging data through LDS: a compiler memory barrier (the hardware returns a
 // wave's LDS accesses in order)
 __device__ __forceinline__ void wave_sync() {
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
                                                         const int* __restrict__ done) {
   if (*done) return;
   constexpr int LD = PNB + 1;
-  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + 32 * (PNB + 2)];
+  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + 32 * (PNB + 2)];  // >= 2 * 64 * (PNB + 2) (update)
   const int kb = min(PNB, n - k0);
   const int t = threadIdx.x;
   if ((int)blockIdx.x >= P) {
@@ -402,9 +404,11 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     }
     const int r0 = st + ti * UT, c0 = st + tj * UT;
     const int nr = min(UT, n + 1 - r0), nc = min(UT, n - c0);
-    double(*A)[LD] = reinterpret_cast<double(*)[LD]>(smem);
-    double(*B)[LD] = reinterpret_cast<double(*)[LD]>(smem + 64 * LD);
-    const int ty = t / 16, tx = t % 16;  // 4x4 outputs per lane
+    constexpr int LU = PNB + 2;  // row pitch: the MFMA fragment reads below are conflict-free
+    double(*A)[LU] = reinterpret_cast<double(*)[LU]>(smem);
+    double(*B)[LU] = reinterpret_cast<double(*)[LU]>(smem + 64 * LU);
+    // matrix cores (v_mfma_f64_16x16x4): wave w owns the 32x32 quadrant (w/2, w%2) = 2x2 MFMA tiles
+    const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3, wy = w >> 1, wx = w & 1;
     {  // 8 + 8 panel loads and the 16 output-tile loads per lane, all issued before any use
       double av[8], bv[8];
 #pragma unroll
@@ -420,42 +424,43 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
         B[i][k] = i < nc ? bv[q] : 0.0;
       }
     }
-    double cold[4][4];
+    double cold[2][2][4];
 #pragma unroll
-    for (int x = 0; x < 4; x++)
+    for (int x = 0; x < 2; x++)
 #pragma unroll
-      for (int y = 0; y < 4; y++)
-        cold[x][y] = H[(size_t)(r0 + min(ty + 16 * x, nr - 1)) * n + c0 + min(tx + 16 * y, nc - 1)];
+      for (int y = 0; y < 2; y++)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          cold[x][y][r] = H[(size_t)(r0 + min(32 * wy + 16 * x + lk + 4 * r, nr - 1)) * n + c0 +
+                            min(32 * wx + 16 * y + lr, nc - 1)];
     __syncthreads();
-    double acc[4][4];
+    d4v acc[2][2];
 #pragma unroll
-    for (int x = 0; x < 4; x++)
+    for (int x = 0; x < 2; x++)
 #pragma unroll
-      for (int y = 0; y < 4; y++) acc[x][y] = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < PNB; k++) {
-      double av[4], bv[4];
+      for (int y = 0; y < 2; y++) acc[x][y] = d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int x = 0; x < 4; x++) av[x] = A[ty + 16 * x][k];
+    for (int q = 0; q < PNB; q += 4) {
+      double fa[2], fb[2];
 #pragma unroll
-      for (int y = 0; y < 4; y++) bv[y] = B[tx + 16 * y][k];
+      for (int x = 0; x < 2; x++) fa[x] = A[32 * wy + 16 * x + lr][q + lk];
 #pragma unroll
-      for (int x = 0; x < 4; x++)
+      for (int y = 0; y < 2; y++) fb[y] = B[32 * wx + 16 * y + lr][q + lk];
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] += av[x] * bv[y];
+      for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 2; y++) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[x], fb[y], acc[x][y], 0, 0, 0);
     }
 #pragma unroll
-    for (int x = 0; x < 4; x++) {
-      const int i = ty + 16 * x;
-      if (i >= nr) continue;
+    for (int x = 0; x < 2; x++)
 #pragma unroll
-      for (int y = 0; y < 4; y++) {
-        const int j = tx + 16 * y;
-        if (j >= nc) continue;
-        if (r0 + i < n && c0 + j > r0 + i) continue;  // strictly-upper part unused
-        H[(size_t)(r0 + i) * n + c0 + j] = cold[x][y] - acc[x][y];
-      }
-    }
+      for (int y = 0; y < 2; y++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int i = 32 * wy + 16 * x + lk + 4 * r, j = 32 * wx + 16 * y + lr;
+          if (i < nr && j < nc && !(r0 + i < n && c0 + j > r0 + i))  // strictly-upper part unused
+            H[(size_t)(r0 + i) * n + c0 + j] = cold[x][y][r] - acc[x][y][r];
+        }
     return;
   }
   // ---- panel s ----
@@ -497,33 +502,31 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     }
   }
   __syncthreads();
+#ifdef CHOL_NOUPD
+  if (false) {
+#else
   if (upd) {  // look-ahead update of this column block by panel s-1
-    {         // A21 rows: thread -> row t/4, columns 8*(t%4) .. +7
-      const int i = t >> 2, j0 = (t & 3) * 8;
-      double acc[8];
+#endif
+    // on the matrix cores (v_mfma_f64_16x16x4): wave w takes rows 16w..16w+15 of A21 (both 16-column
+    // halves) and the 16x16 tile (w/2, w%2) of A11. Operand maps: A[l&15][k=l>>4], B[k=l>>4][l&15];
+    // result row (l>>4)+4r, column l&15. Rows of P1 past kb are zero, so the padding stays zero.
+    const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3;
+    const int ti = w >> 1, tj = w & 1;
+    d4v c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0, cs = c0;
 #pragma unroll
-      for (int m = 0; m < 8; m++) acc[m] = 0.0;
-#pragma unroll 8
-      for (int k = 0; k < PNB; k++) {
-        const double a = LR[i][k];
-#pragma unroll
-        for (int m = 0; m < 8; m++) acc[m] += a * P1[j0 + m][k];
-      }
-#pragma unroll
-      for (int m = 0; m < 8; m++) X[i][j0 + m] -= (j0 + m < kb) ? acc[m] : 0.0;
+    for (int q = 0; q < PNB; q += 4) {
+      const double av = LR[16 * w + lr][q + lk];
+      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1[lr][q + lk], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1[16 + lr][q + lk], c1, 0, 0, 0);
+      cs = __builtin_amdgcn_mfma_f64_16x16x4f64(P1[16 * ti + lr][q + lk], P1[16 * tj + lr][q + lk], cs, 0, 0, 0);
     }
-    {  // A11: thread -> row t/8, columns 4*(t%8) .. +3 (lower part kept)
-      const int i = t >> 3, j0 = (t & 7) * 4;
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-      for (int k = 0; k < PNB; k++) {
-        const double a = P1[i][k];
 #pragma unroll
-        for (int m = 0; m < 4; m++) acc[m] += a * P1[j0 + m][k];
-      }
-#pragma unroll
-      for (int m = 0; m < 4; m++)
-        if (j0 + m <= i) S[i][j0 + m] -= acc[m];
+    for (int r = 0; r < 4; r++) {
+      const int i = 16 * w + lk + 4 * r;
+      X[i][lr] -= c0[r];
+      X[i][16 + lr] -= c1[r];
+      const int si = 16 * ti + lk + 4 * r, sj = 16 * tj + lr;
+      if (sj <= si) S[si][sj] -= cs[r];
     }
     __syncthreads();
   }
@@ -534,7 +537,9 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
 #pragma unroll
       for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
       bool bad = false;
+#ifndef CHOL_NODIAG
       diag_step<0>(r, lane, bad);
+#endif
       if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
       wave_sync();
       if (lane < PNB)
@@ -565,7 +570,9 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
       row0[c] = v.x;
       row0[c + 1] = v.y;
     }
+#ifndef CHOL_NOTRSM
     trsm_pipe<0>(x, Ls, row0);
+#endif
 #pragma unroll
     for (int c = 0; c < PNB; c++) X[lane][c] = x[c];
   }
