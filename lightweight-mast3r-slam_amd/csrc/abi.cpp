@@ -28,7 +28,7 @@ hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*
                                  void*, int*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
-hipError_t m3s_launch_fuse(const void*, int, const FuseArgs*, int, hipStream_t);
+hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
@@ -389,7 +389,8 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     launched += chunk;
     // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
     // before the readback, it runs only if this batch finished the solve (done_chunk == chunk_id)
-    if (do_fuse) HIP_TRY(m3s_launch_fuse(st, chunk_id, &fa, N, s), "track fuse launch");
+    if (do_fuse || !p.direct)
+      HIP_TRY(m3s_launch_fuse(&a, chunk_id, &fa, p.direct ? 0 : 1, N, s), "track fuse launch");
     HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
     HIP_TRY(hipStreamSynchronize(s), "track sync");
     if (hs.done || launched >= p.max_iters) break;

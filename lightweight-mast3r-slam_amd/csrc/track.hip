@@ -33,16 +33,16 @@ namespace m3s {
 __device__ __forceinline__ void sim3_mul_norm(const float* A, const float* B, float* C) {
   float q[4];
   quat_comp(&A[3], &B[3], q);
-  const float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float ni = __builtin_amdgcn_rsqf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   float t[3];
   actSO3(&A[3], &B[0], t);
   C[0] = A[0] + A[7] * t[0];
   C[1] = A[1] + A[7] * t[1];
   C[2] = A[2] + A[7] * t[2];
-  C[3] = q[0] / n;
-  C[4] = q[1] / n;
-  C[5] = q[2] / n;
-  C[6] = q[3] / n;
+  C[3] = q[0] * ni;
+  C[4] = q[1] * ni;
+  C[5] = q[2] * ni;
+  C[6] = q[3] * ni;
   C[7] = A[7] * B[7];
 }
 
@@ -193,14 +193,14 @@ __device__ __forceinline__ void chain_row(const float dh[3], const float Y[3], f
 // themselves are accumulated in fp64; only this tiny serial tail runs in fp32, where div/sqrt are
 // short instruction sequences (the fp64 ones dominated the single-lane tail).
 __device__ bool chol7(const double Hd[7][7], const double gd[7], double tau[7]) {
-  float L[7][7];
+  float L[7][7], Li[7];  // Li = 1 / L_jj (hardware rsq of the pivot: no divides on the chain)
   for (int j = 0; j < 7; j++) {
     float d = (float)Hd[j][j];
     for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
     if (!(d > 0.0f)) return false;
-    d = sqrtf(d);
-    L[j][j] = d;
-    const float dinv = 1.0f / d;
+    const float dinv = __builtin_amdgcn_rsqf(d);
+    L[j][j] = d * dinv;
+    Li[j] = dinv;
     for (int i = j + 1; i < 7; i++) {
       float s = (float)Hd[i][j];
       for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
@@ -211,12 +211,12 @@ __device__ bool chol7(const double Hd[7][7], const double gd[7], double tau[7]) 
   for (int i = 0; i < 7; i++) {
     float s = (float)gd[i];
     for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
-    y[i] = s / L[i][i];
+    y[i] = s * Li[i];
   }
   for (int i = 6; i >= 0; i--) {
     float s = y[i];
     for (int k = i + 1; k < 7; k++) s -= L[k][i] * t[k];
-    t[i] = s / L[i][i];
+    t[i] = s * Li[i];
   }
   for (int i = 0; i < 7; i++) tau[i] = t[i];
   return true;
@@ -255,8 +255,9 @@ __device__ void gn_finish(TrackState* st, const TrackParams& p, const double* su
   for (int c = 0; c < 8; c++) st->T[c] = Tn[c];
   const int it = iter + 1;
   st->iter = it;
-  const double rel = fabs((old - cost) / old);  // inf/inf = nan on the first step -> false
-  const bool conv = (rel < (double)p.rel_error) || (sqrtf(tn2) < p.delta_norm);
+  // |(old - cost) / old| < rel_error without the divide; inf - x < inf * r is false on the first step,
+  // like the reference's inf/inf = nan
+  const bool conv = (fabs(old - cost) < (double)p.rel_error * fabs(old)) || (tn2 < p.delta_norm * p.delta_norm);
   st->old_cost = cost;
   if (conv || it >= p.max_iters) {
     st->status = conv ? M3S_TRACK_OK : M3S_TRACK_MAX_ITERS;
@@ -389,19 +390,6 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
   }
   const int iter0 = st->iter;
   const double old_cost = st->old_cost;
-  if (iter0 == 0 && !p.direct) {
-    // first iteration also counts unique(idx[valid]) (tracker.py:106-108): popcount of the byte map
-    // written by track_setup (flags are 0/1 bytes), one atomic per wave
-    const uint4* fl = reinterpret_cast<const uint4*>(a.flags);
-    const int n16 = (p.N + 15) / 16;
-    int cnt = 0;
-    for (int i = blockIdx.x * GN_THREADS + threadIdx.x; i < n16; i += gridDim.x * GN_THREADS) {
-      const uint4 v = fl[i];
-      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-    }
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&st->n_unique, cnt);
-  }
   if (blockIdx.x == 0) GN_STAMP(0);
   float T[8];
 #pragma unroll
@@ -477,12 +465,34 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
 // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77). Runs only if the
 // GN batch `chunk_id` finished with a pose (so it can be enqueued before the host reads the state
 // back). Out of place like the reference (new X_canon / C tensors); X_out may alias X_in.
+#define FUSE_COUNT_BLOCKS 32
+
 __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id, FuseArgs f,
-                                                   int N) {
-  if (!(st->done && st->done_chunk == chunk_id &&
-        (st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)))
-    return;
+                                                   int N, const uint8_t* __restrict__ flags, int* __restrict__ n_unique) {
+  if (!(st->done && st->done_chunk == chunk_id)) return;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n_unique != nullptr && blockIdx.x < FUSE_COUNT_BLOCKS) {
+    // |unique(idx[valid])| (tracker.py:106-108): popcount of the byte map track_setup wrote (0/1 bytes,
+    // 16-B padded), here after the solve instead of on the first GN iteration's critical path. A few
+    // blocks reduce in LDS and add once each: one device-scope atomic per block, not per wave.
+    __shared__ int s_cnt[4];
+    const uint4* fl = reinterpret_cast<const uint4*>(flags);
+    const int n16 = (N + 15) / 16;
+    int cnt = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += FUSE_COUNT_BLOCKS * 256) {
+      const uint4 v = fl[i];
+      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+      if (tot) atomicAdd(n_unique, tot);
+    }
+  }
+  if (f.X_in == nullptr || !(st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)) return;
   if (n >= N) return;
   float T[8];
 #pragma unroll
@@ -525,9 +535,12 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
   return hipGetLastError();
 }
 
-extern "C" hipError_t m3s_launch_fuse(const void* state, int chunk_id, const FuseArgs* f, int N, hipStream_t s) {
-  hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s,
-                     reinterpret_cast<const TrackState*>(state), chunk_id, *f, N);
+// fusion (f->X_in non-null) and/or the unique-match count (count: the state's n_unique from the byte
+// map) for the GN batch chunk_id that finished
+extern "C" hipError_t m3s_launch_fuse(const TrackArgs* a, int chunk_id, const FuseArgs* f, int count, int N,
+                                      hipStream_t s) {
+  hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
+                     count ? &a->state->n_unique : nullptr);
   return hipGetLastError();
 }
 
