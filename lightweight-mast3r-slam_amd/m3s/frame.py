@@ -26,6 +26,7 @@ class Frame:
     N_updates: int = 0
     K: Optional[torch.Tensor] = None
     score: Optional[torch.Tensor] = None
+    shared: bool = dataclasses.field(default=False, repr=False)  # X_canon / C alias a caller's buffer
 
     def __post_init__(self):
         if self.T_WC is None:
@@ -36,25 +37,32 @@ class Frame:
             return torch.median(C)
         return torch.mean(C)
 
-    def update_pointmap(self, X, C):
-        """frame.py:41-105."""
+    def update_pointmap(self, X, C, own=False):
+        """frame.py:41-105. ``own``: the caller hands over X / C (fresh model outputs nothing else
+        writes), so the first assignment keeps them without the reference's clone; the one in-place
+        mode (indep_conf) copies them before writing."""
         mode = config["tracking"]["filtering_mode"]
         if self.N == 0:
-            self.X_canon, self.C = X.clone(), C.clone()
+            if own:
+                self.X_canon, self.C, self.shared = X, C, True
+            else:
+                self.X_canon, self.C, self.shared = X.clone(), C.clone(), False
             self.N, self.N_updates = 1, 1
             if mode == "best_score":
                 self.score = self.get_score(C)
             return
         if mode == "first":
             if self.N_updates == 1:
-                self.X_canon, self.C, self.N = X.clone(), C.clone(), 1
+                self.X_canon, self.C, self.N, self.shared = X.clone(), C.clone(), 1, False
         elif mode == "recent":
-            self.X_canon, self.C, self.N = X.clone(), C.clone(), 1
+            self.X_canon, self.C, self.N, self.shared = X.clone(), C.clone(), 1, False
         elif mode == "best_score":
             s = self.get_score(C)
             if s > self.score:
-                self.X_canon, self.C, self.N, self.score = X.clone(), C.clone(), 1, s
+                self.X_canon, self.C, self.N, self.score, self.shared = X.clone(), C.clone(), 1, s, False
         elif mode == "indep_conf":
+            if self.shared:  # copy on write: never modify a buffer the frame does not own
+                self.X_canon, self.C, self.shared = self.X_canon.clone(), self.C.clone(), False
             m = C > self.C
             self.X_canon[m.repeat(1, 3)] = X[m.repeat(1, 3)]
             self.C[m] = C[m]
@@ -63,6 +71,7 @@ class Frame:
             self.X_canon = ((self.C * self.X_canon) + (C * X)) / (self.C + C)
             self.C = self.C + C
             self.N += 1
+            self.shared = False
         elif mode == "weighted_spherical":
             def to_sph(P):
                 r = torch.linalg.norm(P, dim=-1, keepdim=True)
@@ -78,6 +87,7 @@ class Frame:
             self.X_canon = to_cart(S)
             self.C = self.C + C
             self.N += 1
+            self.shared = False
         self.N_updates += 1
 
     def get_average_conf(self):

@@ -143,7 +143,7 @@ class FrameTracker:
         self.idx_f2k = idx_f2k
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
-        frame.update_pointmap(Xff, Cff)
+        frame.update_pointmap(Xff, Cff, own=True)  # fresh model outputs: no clone (frame.py:41-45 clones)
 
         use_calib = config["use_calib"]
         img_size = frame_img_size(frame)

@@ -127,6 +127,32 @@ def test_frame_weighted_fusion_matches_reference_formula():
     torch.testing.assert_close(f.get_average_conf(), (C1 + C2) / 2)
 
 
+def test_frame_owned_pointmap_is_copied_before_in_place_modes():
+    """update_pointmap(own=True) keeps the caller's tensors (no clone); indep_conf, the one in-place
+    mode (frame.py:57-61), copies them first, so the caller's buffer is never written."""
+    from m3s.config import config
+    from m3s.frame import Frame
+
+    g = torch.Generator().manual_seed(1)
+    X1, C1 = torch.randn(16, 3, generator=g), torch.rand(16, 1, generator=g) + 1
+    X2, C2 = torch.randn(16, 3, generator=g), torch.rand(16, 1, generator=g) + 2
+    X1_ref, C1_ref = X1.clone(), C1.clone()
+    mode = config["tracking"]["filtering_mode"]
+    try:
+        config["tracking"]["filtering_mode"] = "indep_conf"
+        f = Frame(0, (4, 4))
+        f.update_pointmap(X1, C1, own=True)
+        assert f.X_canon is X1 and f.shared
+        f.update_pointmap(X2, C2)
+        torch.testing.assert_close(X1, X1_ref)  # caller buffer untouched
+        torch.testing.assert_close(C1, C1_ref)
+        m = C2 > C1_ref
+        torch.testing.assert_close(f.X_canon, torch.where(m, X2, X1_ref))
+        assert not f.shared
+    finally:
+        config["tracking"]["filtering_mode"] = mode
+
+
 def test_synthetic_pair_is_consistent():
     from m3s.sim3 import Sim3
     from m3s.synthetic import make_pair
