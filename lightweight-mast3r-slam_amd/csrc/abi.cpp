@@ -444,9 +444,8 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   a->blk_ent = c.take<int>((size_t)4 * E);
   a->rhs_ptr = c.take<int>(Kp + 1);
   a->rhs_ent = c.take<int>((size_t)2 * E);
-  a->H = c.take<double>((size_t)(n + 1) * std::max(n, 1));
+  a->H = c.take<double>((size_t)(2 * n + 1) * std::max(n, 1));  // system, rhs row, carried identity rows
   a->x = c.take<double>(std::max(n, 1));
-  a->Lt = c.take<double>((size_t)((std::max(n, 1) + 31) / 32) * 32 * 32);  // Ldiag: L of every 32x32 diagonal block
   a->dx = c.take<float>(std::max(n, 1));
   a->info = c.take<int>(4);
   a->done = a->info + 1;
@@ -471,7 +470,7 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
   M3S_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "ba: bad shard range");
-  M3S_CHECK((int64_t)(Kp - 1) * 7 <= 8192, "ba: at most 1171 poses (dense system held in LDS by the back solve)");
+  M3S_CHECK((int64_t)(Kp - 1) * 7 <= 8192, "ba: at most 1171 poses");
   if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
                                 "ba calib: height*width must equal the points per keyframe");
   if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");

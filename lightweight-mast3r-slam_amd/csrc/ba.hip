@@ -18,9 +18,11 @@
 //   * ba_assemble: deterministic block-sparse scatter (host-built CSR of contributions per 7x7
 //     block, fixed order) into a dense fp64 [H; g^T] system; every rank therefore solves an
 //     identical system and keeps identical poses.
-//   * dense right-looking blocked fp64 Cholesky (64-wide panels) with the rhs carried as an extra
-//     row (forward substitution for free), blocked back substitution, and the Sim(3) retraction +
-//     |dx| early-exit flag on device: no host synchronisation inside the GN loop.
+//   * dense right-looking blocked fp64 Cholesky (32-wide panels, 16-wide register-row sub-steps
+//     between matrix-core updates) with the rhs and the identity carried as extra rows: the forward
+//     substitution comes for free and the carried identity becomes L^-T, so the back substitution is
+//     one parallel mat-vec; the Sim(3) retraction + |dx| early-exit flag on device: no host
+//     synchronisation inside the GN loop.
 #include "m3s_common.hpp"
 #include "m3s_ba.h"
 
@@ -249,12 +251,17 @@ __global__ void __launch_bounds__(64) ba_edge_kernel(BaArgs a, BaParams p, int E
 // ------------------------------------------------------------------------------------------
 // deterministic assembly: one 64-lane block per nonzero lower 7x7 block (CSR of contributions),
 // rhs rows from the same CSR (sign -1 for the i side, +1 for the j side).
-// Dense system Hs (n+1, n) row-major, row n = g^T (carried through the factorisation).
+// Dense system H (2n+1, n) row-major, row n = g^T, rows n+1.. = identity (carried through the factorisation).
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nblocks) {
+__global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nblocks, int nrhs) {
   if (*a.done) return;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
+  if (b >= nblocks + nrhs) {  // carried identity rows (H row n+1+i = e_i^T)
+    const int i = (b - nblocks - nrhs) * 64 + t;
+    if (i < n) a.H[(size_t)(n + 1 + i) * n + i] = 1.0;
+    return;
+  }
   if (b < nblocks) {
     const int r = a.blk_row[b], c = a.blk_col[b];
     if (t < 49) {
@@ -287,13 +294,20 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 }
 
 // ------------------------------------------------------------------------------------------
-// dense blocked Cholesky, lower, rows 0..n (row n = rhs), columns 0..n-1, right-looking with a
-// one-panel look-ahead: launch s factors panel s (PNB = 32 columns) while panel s-1's trailing
-// update of the columns beyond panel s runs beside it in the same grid. The panel blocks apply
-// panel s-1's update to their own column block first, so the update of the rest of the matrix is
-// off the critical path (one launch per panel instead of a panel launch + an update launch).
+// dense blocked Cholesky with carried inverse rows.
+// H is ((2n+1) x n) row-major: rows 0..n-1 the system (lower triangle used), row n = g^T, row n+1+i =
+// e_i^T. The right-looking factorisation applies its forward elimination to every row below the
+// diagonal, so row n ends as y^T = (L^-1 g)^T and row n+1+i as (L^-1 e_i)^T: the carried block is L^-T
+// and x = L^-T y is one parallel mat-vec (chol_apply_kernel) instead of a serial back substitution.
+// Carried row i stays zero in the columns before i, so it joins the elimination at the panel that
+// holds column i (the "active" carried rows of panel s are i < end of panel s).
+// One launch per PNB-column panel with a one-panel look-ahead: launch s factors panel s while panel
+// s-1's trailing update of the columns beyond panel s runs beside it in the same grid. The panel blocks
+// apply panel s-1's update to their own column block first, so the update of the rest of the matrix
+// is off the critical path.
 // ------------------------------------------------------------------------------------------
 #define PNB 32
+#define SB 16  // sub-panel width of the in-block factorisation (register-row steps between MFMA updates)
 #define UT 64
 
 typedef double d4v __attribute__((ext_vector_type(4)));
@@ -322,88 +336,186 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   return y;
 }
 
-// Right-looking column step J of the register-row diagonal factorisation: pivot and column
-// multipliers broadcast with readlane, rank-1 update of the lane's own row. Rows/columns >= kb are
-// padded with the identity, so every step is valid and the padding stays inert.
-template <int J>
-__device__ __forceinline__ void diag_step(double (&r)[PNB], int lane, bool& bad) {
-  if constexpr (J < PNB) {
+__device__ __forceinline__ double rcp_nr(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  y = fma(y, fma(-d, y, 1.0), y);
+  return fma(y, fma(-d, y, 1.0), y);
+}
+
+// Right-looking column step J of the register-row factorisation of a W-column sub-panel: lane l holds
+// row l (of the sub-panel's rows) in r[0..W); pivot and column multipliers broadcast with readlane,
+// rank-1 update of the lane's own row. Lanes >= W are the rows below the sub-block: the same steps
+// are their triangular solve. Lanes < J only disturb their own strictly-upper entries (never read).
+template <int J, int W>
+__device__ __forceinline__ void diag_step(double (&r)[W], int lane, bool& bad) {
+  if constexpr (J < W) {
     double d = bcast_lane(r[J], J);
     if (!(d > 0.0)) {
       bad = true;
       d = 1.0;
     }
-    const double inv = rsqrt_nr(d);  // 1/sqrt(d): hardware estimate + two Newton steps (serial chain)
+    const double inv = rsqrt_nr(d);  // serial chain: hardware estimate + two Newton steps
     const double sj = d * inv;
-    // unconditional multiplier (a lane-dependent select here makes the allocator spill r[]); lanes
-    // <= J only disturb their own strictly-upper entries, which are never read
+    // unconditional multiplier (a lane-dependent select here makes the allocator spill r[])
     const double l = r[J] * inv;
     r[J] = lane == J ? sj : (lane > J ? l : r[J]);
 #pragma unroll
-    for (int c = J + 1; c < PNB; c++) r[c] -= l * bcast_lane(l, c);
-    diag_step<J + 1>(r, lane, bad);
+    for (int c = J + 1; c < W; c++) r[c] -= l * bcast_lane(l, c);
+    diag_step<J + 1, W>(r, lane, bad);
   }
 }
 
-// Right-looking step J of the register-row forward substitution: x_J *= 1/L_JJ, then fold x_J into
-// the later columns with column J of L11 (row J of Ls = L11^T in LDS). Row J+1 is read from LDS
-// before step J's FMAs (software pipelining: the broadcast reads' latency hides behind them).
-template <int J>
-__device__ __forceinline__ void trsm_pipe(double (&x)[PNB], const double (*Ls)[PNB + 2], const double (&cur)[PNB + 2]) {
-  if constexpr (J < PNB) {
-    double nxt[PNB + 2];
-    if constexpr (J + 1 < PNB) {
+// Right-looking step J of the register-row forward substitution x <- x L^-T over a W-column
+// sub-block: x_J *= 1/L_JJ, then fold x_J into the later columns with column J of L (row J of
+// Ls = L^T, reciprocal pivot stored after the row). Row J+1 is read from LDS before step J's FMAs.
+template <int J, int W>
+__device__ __forceinline__ void trsm_pipe(double (&x)[W], const double (*Ls)[W + 2], const double (&cur)[W + 2]) {
+  if constexpr (J < W) {
+    double nxt[W + 2];
+    if constexpr (J + 1 < W) {
 #pragma unroll
-      for (int c = (J + 2) & ~1; c < PNB + 2; c += 2) {
+      for (int c = (J + 2) & ~1; c < W + 2; c += 2) {
         const double2 v = *reinterpret_cast<const double2*>(&Ls[J + 1][c]);
         nxt[c] = v.x;
         nxt[c + 1] = v.y;
       }
     }
-    x[J] *= cur[PNB];  // reciprocal of the pivot, stored after the row
+    x[J] *= cur[W];
 #pragma unroll
-    for (int k = J + 1; k < PNB; k++) x[k] -= x[J] * cur[k];
-    trsm_pipe<J + 1>(x, Ls, nxt);
+    for (int k = J + 1; k < W; k++) x[k] -= x[J] * cur[k];
+    trsm_pipe<J + 1, W>(x, Ls, nxt);
   }
 }
 
-// Launch s of the factorisation (k0 = s*PNB, kb = panel width). Blocks [0, P): 64 rows each of
-// panel s below its diagonal block (row n = rhs included):
-//   1. coalesced loads of A11 (diagonal block), the block's rows A21 and, for s > 0, the matching
-//      rows of panel s-1 (L_{s,s-1} and L_{R,s-1});
-//   2. s > 0: A11 -= L_{s,s-1} L_{s,s-1}^T, A21 -= L_{R,s-1} L_{s,s-1}^T (the look-ahead update);
-//   3. wave 0 factors A11 (every block redundantly: no extra launch or dependency on the critical
-//      path; lanes = rows in registers, readlane broadcasts), block 0 keeps L11 in Ldiag;
-//   4. wave 0 solves L21 = A21 L11^-T (lane = row) and the block stores it coalesced.
-// Blocks [P, P+U): panel s-1's update A22 -= L21 L21^T over the UTxUT lower tiles of the columns
-// beyond panel s (rows and columns from k0+kb; the lower-triangle tiles enumerated, none idle).
-// L11 never goes back into H; later launches read the diagonal blocks from Ldiag.
-__global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, double* __restrict__ Ldiag, int n,
-                                                        int k0, int P, int* __restrict__ info,
-                                                        const int* __restrict__ done) {
+constexpr int LD = PNB + 1;
+
+// Sub-step C0 of the panel blocks' in-block factorisation (columns C0..C0+SB of the panel):
+//   wave 0: factor rows C0..PNB-1 of the diagonal block on these columns (the rows below the SB x SB
+//           sub-block get their triangular solve from the same register-row steps); publish L_qq^T and
+//           the reciprocal pivots;
+//   then wave 0: S[C0+SB.., C0+SB..] -= L21 L21^T (matrix cores), wave 1: X[:, C0..C0+SB] <- X L_qq^-T;
+//   then all waves: X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T (matrix cores).
+template <int C0>
+__device__ __forceinline__ void panel_substep(double (*S)[LD], double (*X)[LD], double (*Ls)[SB + 2], int t,
+                                              int* info) {
+  constexpr int REST = PNB - C0 - SB;  // columns after this sub-panel
+  if (t < 64) {
+    const int lane = t, row = C0 + lane;
+    double r[SB];
+#pragma unroll
+    for (int c = 0; c < SB; c++) r[c] = row < PNB ? S[row][C0 + c] : 0.0;
+    bool bad = false;
+    diag_step<0, SB>(r, lane, bad);
+    if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
+    wave_sync();
+    if (row < PNB) {
+#pragma unroll
+      for (int c = 0; c < SB; c++) S[row][C0 + c] = (lane < SB && c > lane) ? 0.0 : r[c];
+    }
+    if (lane < SB) {
+#pragma unroll
+      for (int J = 0; J < SB; J++) Ls[J][lane] = J <= lane ? r[J] : 0.0;  // Ls[J][c] = L[c][J]
+      Ls[lane][SB] = rcp_nr(r[lane]);
+      Ls[lane][SB + 1] = 0.0;
+    }
+  }
+  __syncthreads();
+  const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3;
+  if constexpr (REST > 0) {
+    if (w == 0) {  // S22 -= L21 L21^T on the REST x REST lower tiles (16x16 MFMA tiles, K = SB)
+#pragma unroll
+      for (int ti = 0; ti < REST / 16; ti++)
+#pragma unroll
+        for (int tj = 0; tj <= ti; tj++) {
+          d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int q = 0; q < SB; q += 4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(S[C0 + SB + 16 * ti + lr][C0 + q + lk],
+                                                       S[C0 + SB + 16 * tj + lr][C0 + q + lk], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int i = 16 * ti + lk + 4 * r, j = 16 * tj + lr;
+            if (j <= i) S[C0 + SB + i][C0 + SB + j] -= acc[r];
+          }
+        }
+    }
+  }
+  if (w == 1) {  // X[:, C0..C0+SB] <- X L_qq^-T, lane = row
+    const int lane = t - 64;
+    double x[SB], row0[SB + 2];
+#pragma unroll
+    for (int c = 0; c < SB; c++) x[c] = X[lane][C0 + c];
+#pragma unroll
+    for (int c = 0; c < SB + 2; c += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(&Ls[0][c]);
+      row0[c] = v.x;
+      row0[c + 1] = v.y;
+    }
+    trsm_pipe<0, SB>(x, Ls, row0);
+#pragma unroll
+    for (int c = 0; c < SB; c++) X[lane][C0 + c] = x[c];
+  }
+  __syncthreads();
+  if constexpr (REST > 0) {  // X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T: wave w takes rows 16w..16w+15
+#pragma unroll
+    for (int tj = 0; tj < REST / 16; tj++) {
+      d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < SB; q += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[16 * w + lr][C0 + q + lk], S[C0 + SB + 16 * tj + lr][C0 + q + lk],
+                                                   acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; r++) X[16 * w + lk + 4 * r][C0 + SB + 16 * tj + lr] -= acc[r];
+    }
+    __syncthreads();
+  }
+}
+
+// Launch s of the factorisation (k0 = s*PNB, kb = panel width, st = k0 + kb).
+// Blocks [0, P1): 64 rows each of rows st..n (system rows below the diagonal block + the rhs row);
+// blocks [P1, P): 64 rows each of the active carried rows n+1+i, i < st. Each panel block:
+//   1. coalesced loads of A11 (diagonal block), its rows A21 and, for s > 0, the matching rows of
+//      panel s-1 (L_{s,s-1} and L_{R,s-1});
+//   2. s > 0: A11 -= L_{s,s-1} L_{s,s-1}^T, A21 -= L_{R,s-1} L_{s,s-1}^T (the look-ahead update, MFMA);
+//   3. factors A11 redundantly (no extra launch on the critical path) in SB-column sub-steps and solves
+//      its rows L21 = A21 L11^-T along (panel_substep), stores L21 coalesced.
+// Blocks [P, P+U): panel s-1's update A22 -= L21 L21^T over the UTxUT tiles of the columns beyond panel
+// s: lower-triangle tiles of the system rows (+ the rhs row), then full tiles of the carried rows
+// active at panel s-1 (i < k0).
+__global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, int n, int k0, int P1, int P,
+                                                        int* __restrict__ info, const int* __restrict__ done) {
   if (*done) return;
-  constexpr int LD = PNB + 1;
-  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + 32 * (PNB + 2)];  // >= 2 * 64 * (PNB + 2) (update)
+  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + SB * (SB + 2)];  // >= 2 * 64 * (PNB + 2) (update)
   const int kb = min(PNB, n - k0);
+  const int st = k0 + kb;
   const int t = threadIdx.x;
   if ((int)blockIdx.x >= P) {
     // ---- trailing update of panel s-1 (columns PNB wide at kp) beyond panel s ----
-    const int kp = k0 - PNB, st = k0 + kb;
+    const int kp = k0 - PNB;
     const int T = (n - st + UT - 1) / UT;  // column tiles
-    const int tri = T * (T + 1) / 2;
+    const int R = (n + 1 - st + UT - 1) / UT;
+    const int tri = T * (T + 1) / 2, xr = R > T ? T : 0;
     const int u = blockIdx.x - P;
-    int ti, tj;
+    int r0, c0, nr;
     if (u < tri) {
-      ti = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+      int ti = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
       while (ti * (ti + 1) / 2 > u) ti--;
       while ((ti + 1) * (ti + 2) / 2 <= u) ti++;
-      tj = u - ti * (ti + 1) / 2;
-    } else {  // the extra tile row holding only the rhs row (when n - st is a multiple of UT)
-      ti = T;
-      tj = u - tri;
+      const int tj = u - ti * (ti + 1) / 2;
+      r0 = st + ti * UT;
+      c0 = st + tj * UT;
+      nr = min(UT, n + 1 - r0);
+    } else if (u < tri + xr) {  // the extra tile row holding only the rhs row (n - st a multiple of UT)
+      r0 = st + T * UT;
+      c0 = st + (u - tri) * UT;
+      nr = min(UT, n + 1 - r0);
+    } else {  // carried rows active at panel s-1 (i < k0), every column tile
+      const int v = u - tri - xr;
+      r0 = n + 1 + (v / T) * UT;
+      c0 = st + (v % T) * UT;
+      nr = min(UT, n + 1 + k0 - r0);
     }
-    const int r0 = st + ti * UT, c0 = st + tj * UT;
-    const int nr = min(UT, n + 1 - r0), nc = min(UT, n - c0);
+    const int nc = min(UT, n - c0);
     constexpr int LU = PNB + 2;  // row pitch: the MFMA fragment reads below are conflict-free
     double(*A)[LU] = reinterpret_cast<double(*)[LU]>(smem);
     double(*B)[LU] = reinterpret_cast<double(*)[LU]>(smem + 64 * LU);
@@ -465,14 +577,16 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
   }
   // ---- panel s ----
   double(*S)[LD] = reinterpret_cast<double(*)[LD]>(smem);             // A11 -> L11
-  double(*P1)[LD] = reinterpret_cast<double(*)[LD]>(smem + 32 * LD);  // L_{s,s-1}
+  double(*P1s)[LD] = reinterpret_cast<double(*)[LD]>(smem + 32 * LD); // L_{s,s-1}
   double(*X)[LD] = reinterpret_cast<double(*)[LD]>(smem + 64 * LD);   // A21 -> L21 (64 rows)
   double(*LR)[LD] = reinterpret_cast<double(*)[LD]>(smem + 128 * LD); // L_{R,s-1}
-  double(*Ls)[PNB + 2] = reinterpret_cast<double(*)[PNB + 2]>(smem + 192 * LD);
+  double(*Ls)[SB + 2] = reinterpret_cast<double(*)[SB + 2]>(smem + 192 * LD);
   const bool upd = k0 > 0;
   const int kp = k0 - PNB;
-  const int rbase = k0 + kb + blockIdx.x * 64;
-  const int col = t & 31, rs = t >> 5;  // loads: column col of rows rs + 8q
+  const bool carried = (int)blockIdx.x >= P1;
+  const int rbase = carried ? n + 1 + ((int)blockIdx.x - P1) * 64 : st + (int)blockIdx.x * 64;
+  const int rlim = carried ? n + st : n;  // last row of this block's range (inclusive)
+  const int col = t & 31, rs = t >> 5;    // loads: column col of rows rs + 8q
   {
     const int cc = min(col, kb - 1);
     double sv[4], pv[4], xv[8], lv[8];
@@ -484,15 +598,16 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     }
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const int rr = min(rbase + rs + 8 * q, n);
+      const int rr = min(rbase + rs + 8 * q, rlim);
       xv[q] = H[(size_t)rr * n + k0 + cc];
       if (upd) lv[q] = H[(size_t)rr * n + kp + col];
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int i = rs + 8 * q;
-      S[i][col] = (i < kb && col < kb && col <= i) ? sv[q] : 0.0;
-      P1[i][col] = (upd && i < kb) ? pv[q] : 0.0;
+      // rows / columns past kb padded with the identity: the padding stays inert through every step
+      S[i][col] = (i < kb && col < kb) ? (col <= i ? sv[q] : 0.0) : (i == col ? 1.0 : 0.0);
+      P1s[i][col] = (upd && i < kb) ? pv[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -502,11 +617,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     }
   }
   __syncthreads();
-#ifdef CHOL_NOUPD
-  if (false) {
-#else
   if (upd) {  // look-ahead update of this column block by panel s-1
-#endif
     // on the matrix cores (v_mfma_f64_16x16x4): wave w takes rows 16w..16w+15 of A21 (both 16-column
     // halves) and the 16x16 tile (w/2, w%2) of A11. Operand maps: A[l&15][k=l>>4], B[k=l>>4][l&15];
     // result row (l>>4)+4r, column l&15. Rows of P1 past kb are zero, so the padding stays zero.
@@ -516,9 +627,9 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
 #pragma unroll
     for (int q = 0; q < PNB; q += 4) {
       const double av = LR[16 * w + lr][q + lk];
-      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1[lr][q + lk], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1[16 + lr][q + lk], c1, 0, 0, 0);
-      cs = __builtin_amdgcn_mfma_f64_16x16x4f64(P1[16 * ti + lr][q + lk], P1[16 * tj + lr][q + lk], cs, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[lr][q + lk], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[16 + lr][q + lk], c1, 0, 0, 0);
+      cs = __builtin_amdgcn_mfma_f64_16x16x4f64(P1s[16 * ti + lr][q + lk], P1s[16 * tj + lr][q + lk], cs, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -530,142 +641,28 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     }
     __syncthreads();
   }
-  if (t < 64) {
-    const int lane = t, li = min(lane, PNB - 1);
-    {
-      double r[PNB];
-#pragma unroll
-      for (int c = 0; c < PNB; c++) r[c] = (li < kb && c < kb) ? S[li][c] : (c == li ? 1.0 : 0.0);
-      bool bad = false;
-#ifndef CHOL_NODIAG
-      diag_step<0>(r, lane, bad);
-#endif
-      if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
-      wave_sync();
-      if (lane < PNB)
-#pragma unroll
-        for (int c = 0; c < PNB; c++) S[lane][c] = c <= lane ? r[c] : 0.0;
-    }
-    wave_sync();
-    if (lane < PNB) {
-      for (int q = 0; q < PNB; q++) Ls[q][lane] = S[lane][q];  // Ls = L11^T (padded)
-      const double dj = S[lane][lane];
-      double y = __builtin_amdgcn_rcp(dj);  // 1/L_jj: estimate + two Newton steps
-      y = fma(y, fma(-dj, y, 1.0), y);
-      y = fma(y, fma(-dj, y, 1.0), y);
-      Ls[lane][PNB] = y;
-      Ls[lane][PNB + 1] = 0.0;
-      if (blockIdx.x == 0) {
-        double* Ld = Ldiag + (size_t)(k0 / PNB) * PNB * PNB;
-        for (int q = 0; q < PNB; q++) Ld[q * PNB + lane] = S[q][lane];  // row-major L11 (padded)
-      }
-    }
-    wave_sync();
-    double x[PNB], row0[PNB + 2];
-#pragma unroll
-    for (int c = 0; c < PNB; c++) x[c] = X[lane][c];
-#pragma unroll
-    for (int c = 0; c < PNB + 2; c += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(&Ls[0][c]);
-      row0[c] = v.x;
-      row0[c + 1] = v.y;
-    }
-#ifndef CHOL_NOTRSM
-    trsm_pipe<0>(x, Ls, row0);
-#endif
-#pragma unroll
-    for (int c = 0; c < PNB; c++) X[lane][c] = x[c];
-  }
-  __syncthreads();
+  panel_substep<0>(S, X, Ls, t, info);
+  panel_substep<SB>(S, X, Ls, t, info);
 #pragma unroll
   for (int q = 0; q < 8; q++) {
     const int i = rs + 8 * q, rw = rbase + i;
-    if (rw <= n && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
+    if (rw <= rlim && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
   }
 }
 
-// Back substitution L^T x = y (y = row n after the factorisation), one launch per BS_NB-column
-// panel from the end (right-looking):
-//   A (every block, redundantly): load the panel's diagonal block of L into LDS (its PNB-diagonal
-//     blocks from Ldiag) and back-solve it with one wave (lanes hold two unknowns each; x_c broadcast
-//     by readlane, the next row of L prefetched from LDS);
-//   B (block b, columns [b*BS_NB, (b+1)*BS_NB) below k0): y_j -= sum_r L[k0+r][j] x_r, read row-wise
-//     (coalesced) by two half-blocks, written back into row n for the next launch.
-// Replaces a single-block solve that streamed all of L through one CU.
-#define BS_NB 128
-__global__ void __launch_bounds__(1024) chol_back_step_kernel(double* __restrict__ H, const double* __restrict__ Ldiag,
-                                                              double* __restrict__ xg, int n, int k0,
-                                                              const int* __restrict__ done) {
+// x = L^-T y: row i of the carried block (H row n+1+i, zero before column i) dotted with y (row n),
+// one wave per row, fixed summation order (deterministic across ranks).
+__global__ void __launch_bounds__(256) chol_apply_kernel(const double* __restrict__ H, double* __restrict__ x, int n,
+                                                         const int* __restrict__ done) {
   if (*done) return;
-  const int kb = min(BS_NB, n - k0);
-  __shared__ double Ld[BS_NB][BS_NB + 1];
-  __shared__ double rd[BS_NB];
-  __shared__ double xs[BS_NB];
-  __shared__ double part[8][BS_NB];
-  const int t = threadIdx.x;
-  const double* yrow = H + (size_t)n * n;
-  // every global load of the launch is issued up front: the diagonal block (16 per thread) and the
-  // panel rows phase B multiplies (16 per thread; they do not depend on x)
-  double v[16], pb[16];
-#pragma unroll
-  for (int u = 0; u < 16; u++) {
-    const int e = u * 1024 + t, i = e / BS_NB, j = e % BS_NB;
-    const int ic = min(i, kb - 1), jc = min(j, ic);
-    v[u] = (ic / PNB == jc / PNB) ? Ldiag[(size_t)((k0 + ic) / PNB) * PNB * PNB + (ic % PNB) * PNB + (jc % PNB)]
-                                  : H[(size_t)(k0 + ic) * n + k0 + jc];
-  }
-  const int jl = t & (BS_NB - 1), rg = t >> 7;  // phase B: column jl, rows rg + 8u
-  const int j = blockIdx.x * BS_NB + jl;
-  if (k0 > 0) {
-    const int jc = min(j, k0 - 1);
-#pragma unroll
-    for (int u = 0; u < 16; u++) pb[u] = H[(size_t)(k0 + min(rg + 8 * u, kb - 1)) * n + jc];
-  }
-#pragma unroll
-  for (int u = 0; u < 16; u++) {  // rows/columns past kb padded with the identity
-    const int e = u * 1024 + t, i = e / BS_NB, jj = e % BS_NB;
-    Ld[i][jj] = (i < kb && jj <= i) ? v[u] : (i == jj ? 1.0 : 0.0);
-  }
-  __syncthreads();
-  if (t < BS_NB) {
-    const double d = Ld[t][t];
-    double y = __builtin_amdgcn_rcp(d);  // 1/L_cc: estimate + two Newton steps
-    y = fma(y, fma(-d, y, 1.0), y);
-    rd[t] = fma(y, fma(-d, y, 1.0), y);
-  }
-  __syncthreads();
-  if (t < 64) {  // one wave, two unknowns per lane, fully unrolled over the padded 128 columns
-    double y0 = t < kb ? yrow[k0 + t] : 0.0, y1 = t + 64 < kb ? yrow[k0 + t + 64] : 0.0;
-    // L[c][k] = 0 for k > c; k == c only disturbs the finished unknown c
-#pragma unroll 8
-    for (int c = BS_NB - 1; c >= 64; c--) {
-      const double xc = bcast_lane(y1, c - 64) * rd[c];
-      y0 -= Ld[c][t] * xc;
-      y1 -= Ld[c][t + 64] * xc;
-      if (t == 0) xs[c] = xc;
-    }
-#pragma unroll 8
-    for (int c = 63; c >= 0; c--) {
-      const double xc = bcast_lane(y0, c) * rd[c];
-      y0 -= Ld[c][t] * xc;
-      if (t == 0) xs[c] = xc;
-    }
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && t < kb) xg[k0 + t] = xs[t];
-  if (k0 > 0) {
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int u = 0; u < 16; u++) acc[u & 3] += pb[u] * xs[rg + 8 * u];  // xs = 0 past kb
-    part[rg][jl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    __syncthreads();
-    if (t < BS_NB && j < k0) {
-      double sum = 0.0;
-#pragma unroll
-      for (int g = 0; g < 8; g++) sum += part[g][t];
-      H[(size_t)n * n + j] -= sum;
-    }
-  }
+  const int i = (int)((blockIdx.x * 256u + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const double* c = H + (size_t)(n + 1 + i) * n;
+  const double* y = H + (size_t)n * n;
+  double s = 0.0;
+  for (int j = (i & ~63) + lane; j < n; j += 64) s += j >= i ? c[j] * y[j] : 0.0;
+  s = wave_sum(s);
+  if (lane == 0) x[i] = s;
 }
 
 // dx = -x (or 0 when the factorisation failed), poses k >= 1 retracted, |dx| early exit.
@@ -700,6 +697,7 @@ __global__ void __launch_bounds__(256) ba_retr_kernel(BaArgs a, int K, int n, fl
 
 }  // namespace m3s
 
+
 // ------------------------------------------------------------------------------------------
 extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
@@ -718,23 +716,24 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
                                           hipStream_t s) {
   const int n = (K - 1) * 7;
   if (n > 0) {
-    if (hipMemsetAsync(a->H, 0, sizeof(double) * (size_t)(n + 1) * n, s) != hipSuccess) return hipGetLastError();
-    hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows), dim3(64), 0, s, *a, n, nblocks);
+    // system + rhs + carried identity rows (the identity itself is written by the assembly launch)
+    if (hipMemsetAsync(a->H, 0, sizeof(double) * (size_t)(2 * n + 1) * n, s) != hipSuccess) return hipGetLastError();
+    hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nblocks + nrhs_rows + (n + 63) / 64), dim3(64), 0, s, *a, n,
+                       nblocks, nrhs_rows);
     for (int k0 = 0; k0 < n; k0 += PNB) {
       const int kb = n - k0 < PNB ? n - k0 : PNB;
       const int st = k0 + kb;
-      const int P = (n + 1 - st + 63) / 64;  // >= 1: the rhs row
+      const int P1 = (n + 1 - st + 63) / 64;  // >= 1: the rhs row
+      const int P2 = (st + 63) / 64;          // carried rows i < st
       int U = 0;
       if (k0 > 0 && st < n) {
-        const int T = (n - st + UT - 1) / UT, R = (n + 1 - st + UT - 1) / UT;
-        U = T * (T + 1) / 2 + (R > T ? T : 0);
+        const int T = (n - st + UT - 1) / UT, R = (n + 1 - st + UT - 1) / UT, Rc = (k0 + UT - 1) / UT;
+        U = T * (T + 1) / 2 + (R > T ? T : 0) + Rc * T;
       }
-      hipLaunchKernelGGL(m3s::chol_step_kernel, dim3(P + U), dim3(256), 0, s, a->H, a->Lt, n, k0, P, a->info,
+      hipLaunchKernelGGL(m3s::chol_step_kernel, dim3(P1 + P2 + U), dim3(256), 0, s, a->H, n, k0, P1, P1 + P2, a->info,
                          a->done);
     }
-    for (int k0 = ((n - 1) / BS_NB) * BS_NB; k0 >= 0; k0 -= BS_NB)
-      hipLaunchKernelGGL(m3s::chol_back_step_kernel, dim3(k0 > 0 ? (k0 + BS_NB - 1) / BS_NB : 1), dim3(1024), 0, s,
-                         a->H, a->Lt, a->x, n, k0, a->done);
+    hipLaunchKernelGGL(m3s::chol_apply_kernel, dim3((n + 3) / 4), dim3(256), 0, s, a->H, a->x, n, a->done);
   }
   hipLaunchKernelGGL(m3s::ba_retr_kernel, dim3(1), dim3(256), 0, s, *a, K, n, delta_thresh);
   return hipGetLastError();

@@ -36,9 +36,8 @@ struct BaArgs {
   const int* blk_ent;  // edge*2 + (sign<0)
   const int* rhs_ptr;  // (K-1+1)
   const int* rhs_ent;
-  double* H;   // ((n+1), n), n = 7(K-1); row n = rhs
+  double* H;   // ((2n+1), n), n = 7(K-1); row n = rhs, rows n+1.. = carried identity (-> L^-T)
   double* x;   // (n)
-  double* Lt;  // (ceil(n/32), 32, 32) L of every diagonal block (chol_panel -> chol_back_all)
   float* dx;   // (n) output, reference return value
   int* info;   // factorisation failure flag
   int* done;   // early-exit flag (|dx| < delta_thresh)

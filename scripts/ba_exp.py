@@ -56,11 +56,13 @@ if hasattr(lib, "m3s_debug_chol_stamps"):
     buf = (ctypes.c_ulonglong * 512)()
     lib.m3s_debug_chol_stamps(buf)
     npan = min(64, (K - 1) * 7 // 32 + 1)
-    names = ["diag loaded", "diag factored", "Ls ready", "trsm done", "stored"]
+    names = ["loaded", "updated", "diag factored", "trsm done", "stored"]
     acc = [0.0] * 5
     for pnl in range(npan):
         t0 = buf[pnl * 8]
         for k in range(5):
             acc[k] += (buf[pnl * 8 + k + 1] - t0) / 100.0
+    gaps = [(buf[(p + 1) * 8] - buf[p * 8 + 5]) / 100.0 for p in range(npan - 1)]
+    print(f"gap from panel-block-0 store to next launch's block-0 start: mean {sum(gaps) / len(gaps):.2f} us")
     print("panel kernel block 0, mean over panels (us from start): " +
           "  ".join(f"{n}={a / npan:.2f}" for n, a in zip(names, acc)))

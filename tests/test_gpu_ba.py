@@ -175,3 +175,56 @@ def test_single_keyframe_is_a_noop():
     T, dx = _call("rays", Twc0, Xs, np.full((1, N, 1), 2.0, np.float32), np.array([0]), np.array([0]),
                   np.zeros((1, N), np.int64), np.ones((1, N, 1), bool), np.full((1, N, 1), 2.0, np.float32), None, 0, 0)
     assert dx.shape == (0, 7) and np.array_equal(T, Twc0)
+
+
+def _host_solve_from_edge_sums(es, ii, jj):
+    """fp64 host assembly of the pose system from the (E,36) edge-sum table (the rule of
+    gn_kernels.cu:71-113 with pin 1: H_ii += M, H_ij = H_ji -= M, H_jj += M; g_i -= g, g_j += g)
+    and dx = -H^-1 g by numpy (LAPACK)."""
+    u = np.unique(np.concatenate((ii, jj)))
+    ri, rj = np.searchsorted(u, ii) - 1, np.searchsorted(u, jj) - 1
+    n = (len(u) - 1) * 7
+    Hs, g = np.zeros((n, n)), np.zeros(n)
+    iu = np.triu_indices(7)
+    for e in range(es.shape[0]):
+        M = np.zeros((7, 7))
+        M[iu] = es[e, :28]
+        M = M + np.triu(M, 1).T
+        gv = es[e, 28:35]
+        a, b = ri[e], rj[e]
+        if a >= 0:
+            Hs[7 * a:7 * a + 7, 7 * a:7 * a + 7] += M
+            g[7 * a:7 * a + 7] -= gv
+        if b >= 0:
+            Hs[7 * b:7 * b + 7, 7 * b:7 * b + 7] += M
+            g[7 * b:7 * b + 7] += gv
+        if a >= 0 and b >= 0:
+            Hs[7 * a:7 * a + 7, 7 * b:7 * b + 7] -= M
+            Hs[7 * b:7 * b + 7, 7 * a:7 * a + 7] -= M
+    return -np.linalg.solve(Hs, g)
+
+
+@pytest.mark.parametrize("n_kf", [48, 97])
+def test_dense_solve_matches_lapack_on_large_graph(n_kf):
+    """The device factorisation (panels, look-ahead trailing tiles, carried inverse rows, ragged last
+    panel) against LAPACK on the same assembled system: one GN step from the device's own edge sums."""
+    from m3s.config import config
+    from m3s.dist_ba import HipShard, ba_config
+    from m3s.synthetic import make_graph, two_way
+
+    G = make_graph(n_kf=n_kf, H=12, W=16, seed=3)
+    ii, jj, idx, valid, Q = two_way(G)
+    dev = torch.device("cuda")
+    cfg = ba_config("rays", config["local_opt"])
+    Twc = G["Twc0"].to(dev).contiguous()
+    sh = HipShard(cfg, Twc, G["Xs"].to(dev).contiguous(), G["Cs"][..., 0].to(dev).contiguous(), ii.to(dev),
+                  jj.to(dev), idx.to(dev).contiguous(), valid[..., 0].to(dev).contiguous(),
+                  Q[..., 0].to(dev).contiguous(), 0.0, 0, ii.shape[0])
+    sh.linearize()
+    es = sh.edge_sums.view(-1, 36).cpu().numpy().copy()
+    sh.solve()
+    dx = sh.dx.cpu().numpy().reshape(-1)
+    ref = _host_solve_from_edge_sums(es, ii.numpy(), jj.numpy())
+    assert dx.shape == ref.shape == ((n_kf - 1) * 7,)
+    # fp64 factorisation, fp32 output: relative to the step size
+    np.testing.assert_allclose(dx, ref, rtol=0, atol=2e-6 * np.abs(ref).max())
