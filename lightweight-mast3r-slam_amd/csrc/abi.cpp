@@ -31,6 +31,7 @@ hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int
 hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
+hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
 }
 
@@ -435,6 +436,7 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   const int nb_max = Kp + E;
   a->ii_rank = c.take<int>(E);
   a->jj_rank = c.take<int>(E);
+  a->rec = c.take<float4>((size_t)E * N);  // worst case: a shard packs only its own edges
   a->partials = c.take<double>((size_t)E * chunks * 36);
   *es_off = c.off;
   a->edge_sums = c.take<double>((size_t)E * 36);
@@ -574,6 +576,9 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
   P.delta_thresh = delta_thresh;
   P.ws = workspace;
   P.a.dx = dx_out ? dx_out : P.a.dx;
+  // per-call point records of this shard's edges: the matched point, its pixel and the folded validity
+  // weight do not change across GN iterations (only the poses do)
+  HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
   memcpy(plan->opaque, &P, sizeof(P));
   return M3S_OK;
 }

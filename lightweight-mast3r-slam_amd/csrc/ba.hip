@@ -18,7 +18,7 @@
 //   * ba_assemble: deterministic block-sparse scatter (host-built CSR of contributions per 7x7
 //     block, fixed order) into a dense fp64 [H; g^T] system; every rank therefore solves an
 //     identical system and keeps identical poses.
-//   * dense right-looking blocked fp64 Cholesky (32-wide panels, 16-wide register-row sub-steps
+//   * dense right-looking blocked fp64 Cholesky (64-wide panels, 16-wide register-row sub-steps
 //     between matrix-core updates) with the rhs and the identity carried as extra rows: the forward
 //     substitution comes for free and the carried identity becomes L^-T, so the back substitution is
 //     one parallel mat-vec; the Sim(3) retraction + |dx| early-exit flag on device: no host
@@ -58,6 +58,39 @@ __device__ __forceinline__ void acc_local(double* L, double* v, const float J[7]
   }
 }
 
+// Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
+//   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
+//   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
+//   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
+//   gathers, int64 index loads and threshold tests leave the linearisation loop.
+template <int MODE>
+__global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int E_local) {
+  const int N = p.N;
+  const size_t total = (size_t)E_local * N;
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
+    const int e = (int)(o / N), k = (int)(o - (size_t)e * N);
+    const size_t g = (size_t)(e + p.edge_offset) * N + k;
+    const int ix = a.ii_rank[e], jx = a.jj_rank[e];
+    const bool vm = a.valid[g] != 0;
+    const int64_t ind = vm ? a.idx[g] : 0;
+    const float* Xi = a.Xs + ((size_t)ix * N + ind) * 3;
+    const float q = a.Q[g];
+    const bool valid = vm && (q > p.Q_thresh) && (a.Cs[(size_t)ix * N + ind] > p.C_thresh) &&
+                       (a.Cs[(size_t)jx * N + k] > p.C_thresh);
+    // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
+    const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
+    float4 r;
+    if constexpr (MODE == BA_MODE_CALIB) {
+      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
+      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
+      r = make_float4((float)u_t, (float)v_t, Xi[2], sw);
+    } else {
+      r = make_float4(Xi[0], Xi[1], Xi[2], sw);
+    }
+    a.rec[o] = r;
+  }
+}
+
 template <int MODE>  // specialised per residual type: one mode's registers, not the union of three
 __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
   if (*a.done) return;
@@ -77,18 +110,13 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
   for (int c = 0; c < 28; c++) L[c] = 0.0;
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
-  const size_t eoff = (size_t)(e + p.edge_offset) * N;
-  const float* Xi_base = a.Xs + (size_t)ix * N * 3;
+  const float4* rec = a.rec + (size_t)e * N;
   const float* Xj_base = a.Xs + (size_t)jx * N * 3;
-  const float* Ci_base = a.Cs + (size_t)ix * N;
-  const float* Cj_base = a.Cs + (size_t)jx * N;
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
   const int k_end = min(N, k_begin + per);
   for (int k = k_begin + threadIdx.x; k < k_end; k += blockDim.x) {
-    const bool vm = a.valid[eoff + k] != 0;
-    const int64_t ind = vm ? a.idx[eoff + k] : 0;
-    const float Xi[3] = {Xi_base[ind * 3], Xi_base[ind * 3 + 1], Xi_base[ind * 3 + 2]};
+    const float4 R = rec[k];
     const float Xj[3] = {Xj_base[(size_t)k * 3], Xj_base[(size_t)k * 3 + 1], Xj_base[(size_t)k * 3 + 2]};
     float Y[3];
     actSO3(&Tij[3], Xj, Y);  // actSim3 (gn_kernels.cu:207-219): rotate, scale, translate
@@ -98,17 +126,11 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
     Y[0] += Tij[0];
     Y[1] += Tij[1];
     Y[2] += Tij[2];
-    const float q = a.Q[eoff + k];
-    const float ci = Ci_base[ind];
-    const float cj = Cj_base[k];
-    bool valid = vm && (q > p.Q_thresh) && (ci > p.C_thresh) && (cj > p.C_thresh);
-    // hardware sqrt/rsq/rcp (<= 1 ulp) instead of the correctly rounded sequences: the rows are
-    // VALU-bound here and the products are formed in fp64 afterwards; parity is checked against
-    // the fp64 truth (1e-5)
-    const float sqq = __builtin_amdgcn_sqrtf(q);
+    const float sqq = R.w;  // sqrt(q), 0 for an invalid match (ba_pack)
     if constexpr (MODE == BA_MODE_POINTS) {
+      const float Xi[3] = {R.x, R.y, R.z};
       const float err[3] = {Y[0] - Xi[0], Y[1] - Xi[1], Y[2] - Xi[2]};
-      const float sw = valid ? p.inv_a * sqq : 0.0f;
+      const float sw = p.inv_a * sqq;
       const float wc = sw * sw;
       const float J0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
       const float J1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
@@ -117,6 +139,7 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       acc_local<0b1101010>(L, v, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
       acc_local<0b1011100>(L, v, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
     } else if constexpr (MODE == BA_MODE_RAYS) {
+      const float Xi[3] = {R.x, R.y, R.z};
       const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
       const float n1i_inv = __builtin_amdgcn_rsqf(n2i);
       const float n1i = n2i * n1i_inv;
@@ -125,8 +148,8 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       const float n1j = n2j * n1j_inv;
       const float rj[3] = {n1j_inv * Y[0], n1j_inv * Y[1], n1j_inv * Y[2]};
       const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1], rj[2] - n1i_inv * Xi[2], n1j - n1i};
-      const float swr = valid ? p.inv_a * sqq : 0.0f;
-      const float swd = valid ? p.inv_b * sqq : 0.0f;
+      const float swr = p.inv_a * sqq;
+      const float swd = p.inv_b * sqq;
       const float wr = swr * swr, wd = swd * swd;
       const float n3 = n1j_inv * __builtin_amdgcn_rcpf(n2j);
       const float dxx = n1j_inv - Y[0] * Y[0] * n3;
@@ -144,18 +167,17 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       acc_local<0b0011111>(L, v, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
       acc_local<0b1000111>(L, v, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
-      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division instead of 64-bit
-      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
-      const bool valid_z = (Y[2] > p.z_eps) && (Xi[2] > p.z_eps);
+      const float u_t = R.x, v_t = R.y, zi = R.z;
+      const bool valid_z = (Y[2] > p.z_eps) && (zi > p.z_eps);
       const float zj_inv = valid_z ? __builtin_amdgcn_rcpf(Y[2]) : 0.0f;
       const float zj_log = valid_z ? __logf(Y[2]) : 0.0f;
-      const float zi_log = valid_z ? __logf(Xi[2]) : 0.0f;
+      const float zi_log = valid_z ? __logf(zi) : 0.0f;
       const float xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
       const float u = p.fx * xz + p.cx, vv = p.fy * yz + p.cy;
       const bool valid_u = (u > (float)p.pixel_border) && (u < (float)(p.W - 1 - p.pixel_border));
       const bool valid_v = (vv > (float)p.pixel_border) && (vv < (float)(p.H - 1 - p.pixel_border));
-      valid = valid && valid_u && valid_v && valid_z;
-      const float err[3] = {u - (float)u_t, vv - (float)v_t, zj_log - zi_log};
+      const bool valid = valid_u && valid_v && valid_z;
+      const float err[3] = {u - u_t, vv - v_t, zj_log - zi_log};
       const float swp = valid ? p.inv_a * sqq : 0.0f;
       const float swd = valid ? p.inv_b * sqq : 0.0f;
       const float wp = swp * swp, wd = swd * swd;
@@ -301,13 +323,17 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
 // and x = L^-T y is one parallel mat-vec (chol_apply_kernel) instead of a serial back substitution.
 // Carried row i stays zero in the columns before i, so it joins the elimination at the panel that
 // holds column i (the "active" carried rows of panel s are i < end of panel s).
-// One launch per PNB-column panel with a one-panel look-ahead: launch s factors panel s while panel
+// One launch per PNB-column (64) panel with a one-panel look-ahead: launch s factors panel s while panel
 // s-1's trailing update of the columns beyond panel s runs beside it in the same grid. The panel blocks
 // apply panel s-1's update to their own column block first, so the update of the rest of the matrix
 // is off the critical path.
 // ------------------------------------------------------------------------------------------
-#define PNB 32
-#define SB 16  // sub-panel width of the in-block factorisation (register-row steps between MFMA updates)
+#ifndef PNB
+#define PNB 64  // panel width (columns factorised per launch)
+#endif
+#ifndef SB
+#define SB 16  // sub-panel width
+#endif  // of the in-block factorisation (register-row steps between MFMA updates)
 #define UT 64
 
 typedef double d4v __attribute__((ext_vector_type(4)));
@@ -387,95 +413,181 @@ __device__ __forceinline__ void trsm_pipe(double (&x)[W], const double (*Ls)[W +
   }
 }
 
-constexpr int LD = PNB + 1;
+constexpr int LP = PNB + 2;   // LDS row pitch (doubles) of the panel arrays
+constexpr int PR = 64;        // rows per panel block
+constexpr int RS = 256 / PNB;  // rows covered by one pass of the block's 256 loading lanes
 
-// Sub-step C0 of the panel blocks' in-block factorisation (columns C0..C0+SB of the panel):
-//   wave 0: factor rows C0..PNB-1 of the diagonal block on these columns (the rows below the SB x SB
-//           sub-block get their triangular solve from the same register-row steps); publish L_qq^T and
-//           the reciprocal pivots;
-//   then wave 0: S[C0+SB.., C0+SB..] -= L21 L21^T (matrix cores), wave 1: X[:, C0..C0+SB] <- X L_qq^-T;
-//   then all waves: X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T (matrix cores).
+constexpr int NSUB = PNB / SB;  // sub-panels per panel
+
+#ifdef M3S_CHOL_STAMPS  // (experiment builds only) s_memrealtime stamps of panel block 0, per launch
+__device__ unsigned long long g_chol_stamps[64 * 16];
+__shared__ unsigned long long s_stamp[16];
+#define CST(k)                                                                              \
+  do {                                                                                       \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) s_stamp[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define CST(k) \
+  do {         \
+  } while (0)
+#endif
+
+// In-block hand-offs between the waves of one panel block go through LDS words (all waves of a block
+// are resident together). Spins are bounded: a logic error would surface as info = 2 (dx = 0), never
+// as a hung GPU.
+__device__ __forceinline__ void lds_wait_ge(int* f, int v, int* info) {
+  int spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 22)) {
+      *info = 2;
+      break;
+    }
+  }
+}
+
+__device__ __forceinline__ void lds_signal(int* f, int lane) {
+  if (lane == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Wave 0, sub-panel C0: factor rows C0..PNB-1 of the diagonal block on columns C0..C0+SB in registers
+// (the rows below the SB x SB sub-block get their triangular solve from the same steps), write them back
+// to S, publish L_qq^T + reciprocal pivots in Lq; then S[C0+SB.., C0+SB..] -= L21 L21^T (matrix cores).
 template <int C0>
-__device__ __forceinline__ void panel_substep(double (*S)[LD], double (*X)[LD], double (*Ls)[SB + 2], int t,
-                                              int* info) {
-  constexpr int REST = PNB - C0 - SB;  // columns after this sub-panel
-  if (t < 64) {
-    const int lane = t, row = C0 + lane;
+__device__ __forceinline__ void diag_chain(double (*S)[LP], double (*Lq)[SB][SB + 2], int* flags, int lane, int* info) {
+  if constexpr (C0 < PNB) {
+    constexpr int q = C0 / SB, REST = PNB - C0 - SB;
+    const int row = C0 + lane;
     double r[SB];
 #pragma unroll
     for (int c = 0; c < SB; c++) r[c] = row < PNB ? S[row][C0 + c] : 0.0;
     bool bad = false;
     diag_step<0, SB>(r, lane, bad);
     if (bad && lane == 0 && blockIdx.x == 0) *info = 1;
-    wave_sync();
     if (row < PNB) {
 #pragma unroll
       for (int c = 0; c < SB; c++) S[row][C0 + c] = (lane < SB && c > lane) ? 0.0 : r[c];
     }
     if (lane < SB) {
 #pragma unroll
-      for (int J = 0; J < SB; J++) Ls[J][lane] = J <= lane ? r[J] : 0.0;  // Ls[J][c] = L[c][J]
-      Ls[lane][SB] = rcp_nr(r[lane]);
-      Ls[lane][SB + 1] = 0.0;
+      for (int J = 0; J < SB; J++) Lq[q][J][lane] = J <= lane ? r[J] : 0.0;  // Lq[q][J][c] = L[C0+c][C0+J]
+      Lq[q][lane][SB] = rcp_nr(r[lane]);
+      Lq[q][lane][SB + 1] = 0.0;
     }
-  }
-  __syncthreads();
-  const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3;
-  if constexpr (REST > 0) {
-    if (w == 0) {  // S22 -= L21 L21^T on the REST x REST lower tiles (16x16 MFMA tiles, K = SB)
+    lds_signal(&flags[q], lane);  // L_qq and L21 (S columns C0..C0+SB) published
+    CST(3 + q);
+    if constexpr (REST > 0) {
+      // near update: only the next sub-panel's column block (its factorisation waits on it); the far
+      // tiles are updated by waves 2/3 (far_update), which also touch column block q+2 -> wait for
+      // sub-panel q-1's far tiles first
+      if constexpr (q > 0) lds_wait_ge(&flags[4 * NSUB + q - 1], 2, info);
+      const int lr = lane & 15, lk = lane >> 4;
+      double bf[SB / 4];
 #pragma unroll
-      for (int ti = 0; ti < REST / 16; ti++)
+      for (int k = 0; k < SB; k += 4) bf[k / 4] = S[C0 + SB + lr][C0 + k + lk];
 #pragma unroll
-        for (int tj = 0; tj <= ti; tj++) {
-          d4v acc = {0.0, 0.0, 0.0, 0.0};
+      for (int ti = 0; ti < REST / 16; ti++) {
+        d4v acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int q = 0; q < SB; q += 4)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(S[C0 + SB + 16 * ti + lr][C0 + q + lk],
-                                                       S[C0 + SB + 16 * tj + lr][C0 + q + lk], acc, 0, 0, 0);
+        for (int k = 0; k < SB; k += 4)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(S[C0 + SB + 16 * ti + lr][C0 + k + lk], bf[k / 4], acc, 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int i = 16 * ti + lk + 4 * r, j = 16 * tj + lr;
-            if (j <= i) S[C0 + SB + i][C0 + SB + j] -= acc[r];
-          }
+        for (int r4 = 0; r4 < 4; r4++) {
+          const int i = 16 * ti + lk + 4 * r4;
+          if (lr <= i) S[C0 + SB + i][C0 + SB + lr] -= acc[r4];
         }
+      }
     }
+    diag_chain<C0 + SB>(S, Lq, flags, lane, info);
   }
-  if (w == 1) {  // X[:, C0..C0+SB] <- X L_qq^-T, lane = row
-    const int lane = t - 64;
-    double x[SB], row0[SB + 2];
+}
+
+// Waves 2/3, sub-panel C0: the far tiles of S[C0+SB.., C0+SB..] -= L21 L21^T (column blocks q+2..),
+// dealt alternately to the two waves; flags[4 NSUB + q] counts the two waves.
+template <int C0>
+__device__ __forceinline__ void far_update(double (*S)[LP], int* flags, int w, int lane, int* info) {
+  constexpr int q = C0 / SB, RT = (PNB - C0 - SB) / 16;
+  const int lr = lane & 15, lk = lane >> 4;
+  int u = 0;
 #pragma unroll
-    for (int c = 0; c < SB; c++) x[c] = X[lane][C0 + c];
+  for (int ti = 1; ti < RT; ti++)
 #pragma unroll
-    for (int c = 0; c < SB + 2; c += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(&Ls[0][c]);
-      row0[c] = v.x;
-      row0[c + 1] = v.y;
-    }
-    trsm_pipe<0, SB>(x, Ls, row0);
-#pragma unroll
-    for (int c = 0; c < SB; c++) X[lane][C0 + c] = x[c];
-  }
-  __syncthreads();
-  if constexpr (REST > 0) {  // X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T: wave w takes rows 16w..16w+15
-#pragma unroll
-    for (int tj = 0; tj < REST / 16; tj++) {
+    for (int tj = 1; tj <= ti; tj++, u++) {
+      if ((u & 1) != w - 2) continue;
       d4v acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < SB; q += 4)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[16 * w + lr][C0 + q + lk], S[C0 + SB + 16 * tj + lr][C0 + q + lk],
-                                                   acc, 0, 0, 0);
+      for (int k = 0; k < SB; k += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(S[C0 + SB + 16 * ti + lr][C0 + k + lk],
+                                                   S[C0 + SB + 16 * tj + lr][C0 + k + lk], acc, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; r++) X[16 * w + lk + 4 * r][C0 + SB + 16 * tj + lr] -= acc[r];
+      for (int r4 = 0; r4 < 4; r4++) {
+        const int i = 16 * ti + lk + 4 * r4, j = 16 * tj + lr;
+        if (j <= i) S[C0 + SB + i][C0 + SB + j] -= acc[r4];
+      }
     }
-    __syncthreads();
+  lds_signal(&flags[4 * NSUB + q], lane);
+}
+
+// Waves 1..3, sub-panel C0: wave 1 solves X[:, C0..C0+SB] <- X L_qq^-T (lane = row) once L_qq is
+// published and sub-panel q-1's updates of these columns are in; then waves 1..3 apply
+// X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T on their 16-row tiles (wave 1: tiles 0 and 3, waves 2/3: 1/2).
+// flags[q]: L_qq published (wave 0); flags[NSUB + q]: X[:, q] solved (wave 1); flags[2 NSUB + q]:
+// X-update q counts (3 waves); flags[3 NSUB]: look-ahead counts (3 waves); flags[4 NSUB + q]: far
+// S-update q counts (waves 2/3).
+template <int C0>
+__device__ __forceinline__ void row_chain(double (*S)[LP], double (*X)[LP], double (*Lq)[SB][SB + 2], int* flags,
+                                          int w, int lane, int* info) {
+  if constexpr (C0 < PNB) {
+    constexpr int q = C0 / SB, REST = PNB - C0 - SB;
+    if (w == 1) {
+      lds_wait_ge(&flags[q], 1, info);
+      lds_wait_ge(q == 0 ? &flags[3 * NSUB] : &flags[2 * NSUB + q - 1], 3, info);
+      double x[SB], row0[SB + 2];
+#pragma unroll
+      for (int c = 0; c < SB; c++) x[c] = X[lane][C0 + c];
+#pragma unroll
+      for (int c = 0; c < SB + 2; c += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(&Lq[q][0][c]);
+        row0[c] = v.x;
+        row0[c + 1] = v.y;
+      }
+      trsm_pipe<0, SB>(x, Lq[q], row0);
+#pragma unroll
+      for (int c = 0; c < SB; c++) X[lane][C0 + c] = x[c];
+      lds_signal(&flags[NSUB + q], lane);
+      CST(9 + q);
+    } else {
+      if constexpr (PNB - C0 - SB > 16) {
+        lds_wait_ge(&flags[q], 1, info);
+        far_update<C0>(S, flags, w, lane, info);
+      }
+      lds_wait_ge(&flags[NSUB + q], 1, info);
+    }
+    if constexpr (REST > 0) {
+      const int lr = lane & 15, lk = lane >> 4;
+      for (int rt = w - 1; rt < PR / 16; rt += 3) {
+#pragma unroll
+        for (int tj = 0; tj < REST / 16; tj++) {
+          d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int k = 0; k < SB; k += 4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[16 * rt + lr][C0 + k + lk], S[C0 + SB + 16 * tj + lr][C0 + k + lk],
+                                                       acc, 0, 0, 0);
+#pragma unroll
+          for (int r4 = 0; r4 < 4; r4++) X[16 * rt + lk + 4 * r4][C0 + SB + 16 * tj + lr] -= acc[r4];
+        }
+      }
+      lds_signal(&flags[2 * NSUB + q], lane);
+    }
+    row_chain<C0 + SB>(S, X, Lq, flags, w, lane, info);
   }
 }
 
 // Launch s of the factorisation (k0 = s*PNB, kb = panel width, st = k0 + kb).
-// Blocks [0, P1): 64 rows each of rows st..n (system rows below the diagonal block + the rhs row);
-// blocks [P1, P): 64 rows each of the active carried rows n+1+i, i < st. Each panel block:
+// Blocks [0, P1): PR rows each of rows st..n (system rows below the diagonal block + the rhs row);
+// blocks [P1, P): PR rows each of the active carried rows n+1+i, i < st. Each panel block:
 //   1. coalesced loads of A11 (diagonal block), its rows A21 and, for s > 0, the matching rows of
-//      panel s-1 (L_{s,s-1} and L_{R,s-1});
+//      panel s-1 (L_{s,s-1} and L_{R,s-1}), all in flight at once;
 //   2. s > 0: A11 -= L_{s,s-1} L_{s,s-1}^T, A21 -= L_{R,s-1} L_{s,s-1}^T (the look-ahead update, MFMA);
 //   3. factors A11 redundantly (no extra launch on the critical path) in SB-column sub-steps and solves
 //      its rows L21 = A21 L11^-T along (panel_substep), stores L21 coalesced.
@@ -484,8 +596,10 @@ __device__ __forceinline__ void panel_substep(double (*S)[LD], double (*X)[LD], 
 // active at panel s-1 (i < k0).
 __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, int n, int k0, int P1, int P,
                                                         int* __restrict__ info, const int* __restrict__ done) {
+  if (threadIdx.x < 64) CST(0);
   if (*done) return;
-  __shared__ double smem[2 * 32 * LD + 2 * 64 * LD + SB * (SB + 2)];  // >= 2 * 64 * (PNB + 2) (update)
+  static_assert(UT == 64 && PR == 64 && PNB % 16 == 0 && 256 % PNB == 0, "tiling");
+  __shared__ double smem[2 * PNB * LP + 2 * PR * LP + NSUB * SB * (SB + 2) + 3 * NSUB];  // >= 2 * UT * LP (update tiles)
   const int kb = min(PNB, n - k0);
   const int st = k0 + kb;
   const int t = threadIdx.x;
@@ -516,21 +630,21 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
       nr = min(UT, n + 1 + k0 - r0);
     }
     const int nc = min(UT, n - c0);
-    constexpr int LU = PNB + 2;  // row pitch: the MFMA fragment reads below are conflict-free
-    double(*A)[LU] = reinterpret_cast<double(*)[LU]>(smem);
-    double(*B)[LU] = reinterpret_cast<double(*)[LU]>(smem + 64 * LU);
+    double(*A)[LP] = reinterpret_cast<double(*)[LP]>(smem);
+    double(*B)[LP] = reinterpret_cast<double(*)[LP]>(smem + UT * LP);
     // matrix cores (v_mfma_f64_16x16x4): wave w owns the 32x32 quadrant (w/2, w%2) = 2x2 MFMA tiles
     const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3, wy = w >> 1, wx = w & 1;
-    {  // 8 + 8 panel loads and the 16 output-tile loads per lane, all issued before any use
-      double av[8], bv[8];
+    constexpr int NQ = UT * PNB / 256;
+    {  // the panel loads and the 16 output-tile loads per lane, all issued before any use
+      double av[NQ], bv[NQ];
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
+      for (int q = 0; q < NQ; q++) {
         const int e = t + 256 * q, i = e / PNB, k = e % PNB;
         av[q] = H[(size_t)(r0 + min(i, nr - 1)) * n + kp + k];
         bv[q] = H[(size_t)(c0 + min(i, nc - 1)) * n + kp + k];
       }
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
+      for (int q = 0; q < NQ; q++) {
         const int e = t + 256 * q, i = e / PNB, k = e % PNB;
         A[i][k] = i < nr ? av[q] : 0.0;
         B[i][k] = i < nc ? bv[q] : 0.0;
@@ -576,78 +690,126 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
     return;
   }
   // ---- panel s ----
-  double(*S)[LD] = reinterpret_cast<double(*)[LD]>(smem);             // A11 -> L11
-  double(*P1s)[LD] = reinterpret_cast<double(*)[LD]>(smem + 32 * LD); // L_{s,s-1}
-  double(*X)[LD] = reinterpret_cast<double(*)[LD]>(smem + 64 * LD);   // A21 -> L21 (64 rows)
-  double(*LR)[LD] = reinterpret_cast<double(*)[LD]>(smem + 128 * LD); // L_{R,s-1}
-  double(*Ls)[SB + 2] = reinterpret_cast<double(*)[SB + 2]>(smem + 192 * LD);
+  double(*S)[LP] = reinterpret_cast<double(*)[LP]>(smem);                  // A11 -> L11
+  double(*P1s)[LP] = reinterpret_cast<double(*)[LP]>(smem + PNB * LP);     // L_{s,s-1}
+  double(*X)[LP] = reinterpret_cast<double(*)[LP]>(smem + 2 * PNB * LP);   // A21 -> L21 (PR rows)
+  double(*LR)[LP] = reinterpret_cast<double(*)[LP]>(smem + (2 * PNB + PR) * LP);  // L_{R,s-1}
+  double(*Lq)[SB][SB + 2] = reinterpret_cast<double(*)[SB][SB + 2]>(smem + 2 * (PNB + PR) * LP);
+  int* flags = reinterpret_cast<int*>(smem + 2 * (PNB + PR) * LP + NSUB * SB * (SB + 2));  // 5 NSUB words
+  if (t < 5 * NSUB) flags[t] = 0;
   const bool upd = k0 > 0;
   const int kp = k0 - PNB;
   const bool carried = (int)blockIdx.x >= P1;
-  const int rbase = carried ? n + 1 + ((int)blockIdx.x - P1) * 64 : st + (int)blockIdx.x * 64;
+  const int rbase = carried ? n + 1 + ((int)blockIdx.x - P1) * PR : st + (int)blockIdx.x * PR;
   const int rlim = carried ? n + st : n;  // last row of this block's range (inclusive)
-  const int col = t & 31, rs = t >> 5;    // loads: column col of rows rs + 8q
+  const int col = t % PNB, rs = t / PNB;  // loads: column col of rows rs + RS q
   {
+    constexpr int QS = PNB / RS, QX = PR / RS;
     const int cc = min(col, kb - 1);
-    double sv[4], pv[4], xv[8], lv[8];
+    double sv[QS], pv[QS], xv[QX], lv[QX];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int rr = k0 + min(rs + 8 * q, kb - 1);
+    for (int q = 0; q < QS; q++) {
+      const int rr = k0 + min(rs + RS * q, kb - 1);
       sv[q] = H[(size_t)rr * n + k0 + cc];
       if (upd) pv[q] = H[(size_t)rr * n + kp + col];
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int rr = min(rbase + rs + 8 * q, rlim);
+    for (int q = 0; q < QX; q++) {
+      const int rr = min(rbase + rs + RS * q, rlim);
       xv[q] = H[(size_t)rr * n + k0 + cc];
       if (upd) lv[q] = H[(size_t)rr * n + kp + col];
     }
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int i = rs + 8 * q;
+    for (int q = 0; q < QS; q++) {
+      const int i = rs + RS * q;
       // rows / columns past kb padded with the identity: the padding stays inert through every step
       S[i][col] = (i < kb && col < kb) ? (col <= i ? sv[q] : 0.0) : (i == col ? 1.0 : 0.0);
       P1s[i][col] = (upd && i < kb) ? pv[q] : 0.0;
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int i = rs + 8 * q;
+    for (int q = 0; q < QX; q++) {
+      const int i = rs + RS * q;
       X[i][col] = col < kb ? xv[q] : 0.0;
       LR[i][col] = upd ? lv[q] : 0.0;
     }
   }
   __syncthreads();
-  if (upd) {  // look-ahead update of this column block by panel s-1
-    // on the matrix cores (v_mfma_f64_16x16x4): wave w takes rows 16w..16w+15 of A21 (both 16-column
-    // halves) and the 16x16 tile (w/2, w%2) of A11. Operand maps: A[l&15][k=l>>4], B[k=l>>4][l&15];
-    // result row (l>>4)+4r, column l&15. Rows of P1 past kb are zero, so the padding stays zero.
-    const int w = t >> 6, lr = t & 15, lk = (t >> 4) & 3;
-    const int ti = w >> 1, tj = w & 1;
-    d4v c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0, cs = c0;
+  if (t < 64) CST(1);
+  const int w = t >> 6, lane = t & 63, lr = t & 15, lk = (t >> 4) & 3;
+  if (upd) {  // look-ahead update of the diagonal block by panel s-1: A11 -= L_{s,s-1} L_{s,s-1}^T
+    // (matrix cores, v_mfma_f64_16x16x4; operand maps A[l&15][k=l>>4], B[k=l>>4][l&15]; result row
+    // (l>>4)+4r, column l&15): the lower 16x16 tiles u = w, w+4, .. per wave
+    constexpr int CT = PNB / 16, NT = CT * (CT + 1) / 2;
 #pragma unroll
-    for (int q = 0; q < PNB; q += 4) {
-      const double av = LR[16 * w + lr][q + lk];
-      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[lr][q + lk], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[16 + lr][q + lk], c1, 0, 0, 0);
-      cs = __builtin_amdgcn_mfma_f64_16x16x4f64(P1s[16 * ti + lr][q + lk], P1s[16 * tj + lr][q + lk], cs, 0, 0, 0);
+    for (int uu = 0; uu < NT; uu += 4) {
+      const int u = uu + w;
+      if (u < NT) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= u) ti++;
+        const int tj = u - ti * (ti + 1) / 2;
+        double fa[PNB / 4], fb[PNB / 4];  // every operand read issued before the MFMA chain
+#pragma unroll
+        for (int q = 0; q < PNB; q += 4) {
+          fa[q / 4] = P1s[16 * ti + lr][q + lk];
+          fb[q / 4] = P1s[16 * tj + lr][q + lk];
+        }
+        d4v c2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};  // two interleaved chains
+#pragma unroll
+        for (int q = 0; q < PNB / 4; q++)
+          c2[q & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c2[q & 1], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int si = 16 * ti + lk + 4 * r, sj = 16 * tj + lr;
+          if (sj <= si) S[si][sj] -= c2[0][r] + c2[1][r];
+        }
+      }
     }
+  }
+  __syncthreads();  // diagonal block complete, flags zeroed
+  if (w == 0) {
+    CST(2);
+    diag_chain<0>(S, Lq, flags, lane, info);  // the serial chain runs ahead on its own wave
+    CST(7);
+  } else {
+    if (upd) {  // look-ahead update of this block's rows: A21 -= L_{R,s-1} L_{s,s-1}^T (rows split 3 ways)
+      constexpr int CT = PNB / 16;
+      for (int rt = w - 1; rt < PR / 16; rt += 3) {
+        d4v cx[CT];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int i = 16 * w + lk + 4 * r;
-      X[i][lr] -= c0[r];
-      X[i][16 + lr] -= c1[r];
-      const int si = 16 * ti + lk + 4 * r, sj = 16 * tj + lr;
-      if (sj <= si) S[si][sj] -= cs[r];
+        for (int j = 0; j < CT; j++) cx[j] = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < PNB; q += 4) {
+          const double av = LR[16 * rt + lr][q + lk];
+#pragma unroll
+          for (int j = 0; j < CT; j++)
+            cx[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[16 * j + lr][q + lk], cx[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < CT; j++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) X[16 * rt + lk + 4 * r][16 * j + lr] -= cx[j][r];
+      }
     }
-    __syncthreads();
+    lds_signal(&flags[3 * NSUB], lane);
+    if (w == 1) CST(8);
+    row_chain<0>(S, X, Lq, flags, w, lane, info);
   }
-  panel_substep<0>(S, X, Ls, t, info);
-  panel_substep<SB>(S, X, Ls, t, info);
+  __syncthreads();
+  if (w == 0) CST(13);
+  {
+    constexpr int QX = PR / RS;
 #pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const int i = rs + 8 * q, rw = rbase + i;
-    if (rw <= rlim && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
+    for (int q = 0; q < QX; q++) {
+      const int i = rs + RS * q, rw = rbase + i;
+      if (rw <= rlim && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
+    }
   }
+#ifdef M3S_CHOL_STAMPS
+  if (blockIdx.x == 0 && t == 0 && k0 / PNB < 64) {
+    s_stamp[14] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 16; k++) g_chol_stamps[(k0 / PNB) * 16 + k] = s_stamp[k];
+  }
+#endif
 }
 
 // x = L^-T y: row i of the carried block (H row n+1+i, zero before column i) dotted with y (row n),
@@ -697,8 +859,28 @@ __global__ void __launch_bounds__(256) ba_retr_kernel(BaArgs a, int K, int n, fl
 
 }  // namespace m3s
 
+#ifdef M3S_CHOL_STAMPS
+extern "C" int m3s_debug_chol_stamps(unsigned long long* out) {
+  (void)hipDeviceSynchronize();
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_chol_stamps), sizeof(unsigned long long) * 1024) == hipSuccess ? 0 : -1;
+}
+#endif
+
 
 // ------------------------------------------------------------------------------------------
+extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
+  if (E_local <= 0) return hipSuccess;
+  const size_t total = (size_t)E_local * p->N;
+  const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
+  if (p->mode == BA_MODE_CALIB)
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, E_local);
+  else if (p->mode == BA_MODE_RAYS)
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, E_local);
+  else
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, E_local);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
   const dim3 g(E_local * p->chunks);
@@ -723,8 +905,8 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nblocks, i
     for (int k0 = 0; k0 < n; k0 += PNB) {
       const int kb = n - k0 < PNB ? n - k0 : PNB;
       const int st = k0 + kb;
-      const int P1 = (n + 1 - st + 63) / 64;  // >= 1: the rhs row
-      const int P2 = (st + 63) / 64;          // carried rows i < st
+      const int P1 = (n + 1 - st + m3s::PR - 1) / m3s::PR;  // >= 1: the rhs row
+      const int P2 = (st + m3s::PR - 1) / m3s::PR;          // carried rows i < st
       int U = 0;
       if (k0 > 0 && st < n) {
         const int T = (n - st + UT - 1) / UT, R = (n + 1 - st + UT - 1) / UT, Rc = (k0 + UT - 1) / UT;

@@ -1,6 +1,7 @@
 // Internal (non-ABI) structs shared by ba.hip and abi.cpp. The public C ABI is include/m3s.h.
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 
 #define BA_MODE_POINTS 0
 #define BA_MODE_RAYS 1
@@ -27,6 +28,7 @@ struct BaArgs {
   const int64_t* idx;    // (E,N) global edge rows
   const uint8_t* valid;  // (E,N)
   const float* Q;        // (E,N)
+  float4* rec;           // (E_local, N) per-call point records (ba_pack): {Xi | u_t, v_t, z_i ; sqrt-weight}
   double* partials;      // (E_local*chunks, 36)
   double* edge_sums;     // (E, 36) global edge rows; all-reduced across ranks in multi-GPU BA
   // assembly CSR (host-built once per call)

@@ -53,16 +53,15 @@ for rep in range(2):
           f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}", flush=True)
 
 if hasattr(lib, "m3s_debug_chol_stamps"):
-    buf = (ctypes.c_ulonglong * 512)()
+    buf = (ctypes.c_ulonglong * 1024)()
     lib.m3s_debug_chol_stamps(buf)
-    npan = min(64, (K - 1) * 7 // 32 + 1)
-    names = ["loaded", "updated", "diag factored", "trsm done", "stored"]
-    acc = [0.0] * 5
-    for pnl in range(npan):
-        t0 = buf[pnl * 8]
-        for k in range(5):
-            acc[k] += (buf[pnl * 8 + k + 1] - t0) / 100.0
-    gaps = [(buf[(p + 1) * 8] - buf[p * 8 + 5]) / 100.0 for p in range(npan - 1)]
-    print(f"gap from panel-block-0 store to next launch's block-0 start: mean {sum(gaps) / len(gaps):.2f} us")
-    print("panel kernel block 0, mean over panels (us from start): " +
-          "  ".join(f"{n}={a / npan:.2f}" for n, a in zip(names, acc)))
+    n = (K - 1) * 7
+    npan = min(64, (n + 63) // 64)
+    names = {1: "loaded", 2: "diag look-ahead", 3: "L0", 4: "L1", 5: "L2", 6: "L3", 7: "chain end", 8: "X look-ahead",
+             9: "T0", 10: "T1", 11: "T2", 12: "T3", 13: "synced", 14: "stored"}
+    for sel in (range(1, 2), range(npan // 2, npan // 2 + 1), range(npan - 1, npan)):
+        for p in sel:
+            t0 = buf[p * 16]
+            print(f"panel {p}: " + "  ".join(f"{nm}={(buf[p * 16 + k] - t0) / 100.0:.2f}" for k, nm in names.items()))
+    gaps = [(buf[(p + 1) * 16] - buf[p * 16 + 14]) / 100.0 for p in range(npan - 1)]
+    print(f"gap from panel-block-0 end to next launch's block-0 start: mean {sum(gaps) / len(gaps):.2f} us")
