@@ -352,19 +352,17 @@ __device__ __forceinline__ double bcast_lane(double v, int src) {
   return *reinterpret_cast<double*>(&x);
 }
 
-// 1/sqrt(d) for d > 0 to ~1 ulp: v_rsq_f64 estimate refined by two Newton steps — a fraction of the
-// latency of the correctly rounded sqrt + divide sequences on the pivot chain.
+// 1/sqrt(d) and 1/d for d > 0: the v_rsq_f64 / v_rcp_f64 estimates (~2^-22 relative) refined by ONE
+// Newton step (~2^-44): the pivot chain is latency-bound (a dependent v_fma_f64 costs ~13 ns on gfx950,
+// measured by scripts/micro/mfma_f64.hip), and 1e-13 relative pivots are far inside the 1e-5 pose
+// contract (the LAPACK parity test bounds the solve at 2e-6 of the step).
 __device__ __forceinline__ double rsqrt_nr(double d) {
-  double y = __builtin_amdgcn_rsq(d);
-  const double h = 0.5 * d;
-#pragma unroll
-  for (int it = 0; it < 2; it++) y = fma(y, fma(-h * y, y, 0.5), y);
-  return y;
+  const double y = __builtin_amdgcn_rsq(d);
+  return fma(y, fma(-0.5 * d * y, y, 0.5), y);
 }
 
 __device__ __forceinline__ double rcp_nr(double d) {
-  double y = __builtin_amdgcn_rcp(d);
-  y = fma(y, fma(-d, y, 1.0), y);
+  const double y = __builtin_amdgcn_rcp(d);
   return fma(y, fma(-d, y, 1.0), y);
 }
 
@@ -450,6 +448,25 @@ __device__ __forceinline__ void lds_signal(int* f, int lane) {
   if (lane == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Look-ahead tile (ti, tj) of the diagonal block: S[16ti.., 16tj..] -= P1 P1^T (K = PNB), operand reads
+// issued before the MFMA chain, two interleaved accumulators.
+__device__ __forceinline__ void la_tile(double (*S)[LP], const double (*P1)[LP], int ti, int tj, int lr, int lk) {
+  double fa[PNB / 4], fb[PNB / 4];
+#pragma unroll
+  for (int q = 0; q < PNB; q += 4) {
+    fa[q / 4] = P1[16 * ti + lr][q + lk];
+    fb[q / 4] = P1[16 * tj + lr][q + lk];
+  }
+  d4v c2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+  for (int q = 0; q < PNB / 4; q++) c2[q & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c2[q & 1], 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int si = 16 * ti + lk + 4 * r, sj = 16 * tj + lr;
+    if (sj <= si) S[si][sj] -= c2[0][r] + c2[1][r];
+  }
+}
+
 // Wave 0, sub-panel C0: factor rows C0..PNB-1 of the diagonal block on columns C0..C0+SB in registers
 // (the rows below the SB x SB sub-block get their triangular solve from the same steps), write them back
 // to S, publish L_qq^T + reciprocal pivots in Lq; then S[C0+SB.., C0+SB..] -= L21 L21^T (matrix cores).
@@ -478,9 +495,10 @@ __device__ __forceinline__ void diag_chain(double (*S)[LP], double (*Lq)[SB][SB 
     CST(3 + q);
     if constexpr (REST > 0) {
       // near update: only the next sub-panel's column block (its factorisation waits on it); the far
-      // tiles are updated by waves 2/3 (far_update), which also touch column block q+2 -> wait for
+      // tiles are updated by waves 1/2 (far_update), which also touch column block q+2 -> wait for
       // sub-panel q-1's far tiles first
       if constexpr (q > 0) lds_wait_ge(&flags[4 * NSUB + q - 1], 2, info);
+      else lds_wait_ge(&flags[5 * NSUB], 3, info);  // the look-ahead of the later column blocks is in
       const int lr = lane & 15, lk = lane >> 4;
       double bf[SB / 4];
 #pragma unroll
@@ -502,7 +520,7 @@ __device__ __forceinline__ void diag_chain(double (*S)[LP], double (*Lq)[SB][SB 
   }
 }
 
-// Waves 2/3, sub-panel C0: the far tiles of S[C0+SB.., C0+SB..] -= L21 L21^T (column blocks q+2..),
+// Waves 1/2, sub-panel C0: the far tiles of S[C0+SB.., C0+SB..] -= L21 L21^T (column blocks q+2..),
 // dealt alternately to the two waves; flags[4 NSUB + q] counts the two waves.
 template <int C0>
 __device__ __forceinline__ void far_update(double (*S)[LP], int* flags, int w, int lane, int* info) {
@@ -513,7 +531,7 @@ __device__ __forceinline__ void far_update(double (*S)[LP], int* flags, int w, i
   for (int ti = 1; ti < RT; ti++)
 #pragma unroll
     for (int tj = 1; tj <= ti; tj++, u++) {
-      if ((u & 1) != w - 2) continue;
+      if ((u & 1) != w - 1) continue;
       d4v acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < SB; k += 4)
@@ -528,20 +546,71 @@ __device__ __forceinline__ void far_update(double (*S)[LP], int* flags, int w, i
   lds_signal(&flags[4 * NSUB + q], lane);
 }
 
-// Waves 1..3, sub-panel C0: wave 1 solves X[:, C0..C0+SB] <- X L_qq^-T (lane = row) once L_qq is
-// published and sub-panel q-1's updates of these columns are in; then waves 1..3 apply
-// X[:, C0+SB..] -= X[:, C0..C0+SB] L21^T on their 16-row tiles (wave 1: tiles 0 and 3, waves 2/3: 1/2).
-// flags[q]: L_qq published (wave 0); flags[NSUB + q]: X[:, q] solved (wave 1); flags[2 NSUB + q]:
-// X-update q counts (3 waves); flags[3 NSUB]: look-ahead counts (3 waves); flags[4 NSUB + q]: far
-// S-update q counts (waves 2/3).
+// Row side (waves 1..3) of the panel block. Row tiles (16 rows of X) are owned by one wave each
+// (wave 1: tiles 0 and 2, wave 2: tiles 1 and 3; wave 3 only solves), so every element's update order
+// is fixed (deterministic). Per column block j, R[j] = flags[2 NSUB + j] counts the finished contributions:
+// the look-ahead of panel s-1 (la_rows<j>) and the X-updates of sub-panels p < j, one signal per wave
+// each; wave 3 solves X[:, block q] <- X L_qq^-T (lane = row) once L_qq is published (flags[q]) and
+// R[q] = 3 (q + 1), then signals flags[NSUB + q]. Each wave then looks ahead on block q+1 and applies
+// sub-panel q's update to its row tiles: block q+1 first (the next solve waits on it), then the rest.
+// flags: [q] L_qq published (wave 0); [NSUB + q] block q solved (wave 3); [2 NSUB + j] R[j];
+// [4 NSUB + q] far S-update q (waves 2/3); [5 NSUB] the diagonal block's later look-ahead tiles.
+__device__ __forceinline__ bool owns_tile(int w, int rt) { return w <= 2 && (rt & 1) == w - 1; }
+
+template <int J>
+__device__ __forceinline__ void la_rows(double (*X)[LP], const double (*LR)[LP], const double (*P1)[LP], int* flags, int w,
+                                        int lane, bool upd) {
+  const int lr = lane & 15, lk = lane >> 4;
+  if (upd) {  // X[own rows][block J] -= L_{R,s-1} L_{s,s-1}[block J]^T
+#pragma unroll
+    for (int rt = 0; rt < PR / 16; rt++) {
+      if (!owns_tile(w, rt)) continue;
+      d4v c2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+      for (int q = 0; q < PNB; q += 4)
+        c2[(q >> 2) & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(LR[16 * rt + lr][q + lk], P1[16 * J + lr][q + lk],
+                                                                c2[(q >> 2) & 1], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; r++) X[16 * rt + lk + 4 * r][16 * J + lr] -= c2[0][r] + c2[1][r];
+    }
+  }
+  lds_signal(&flags[2 * NSUB + J], lane);
+}
+
+// X[own rows][block J] -= X[own rows][block q] L[block J rows][block q]^T, then R[J] += 1
+template <int C0, int J>
+__device__ __forceinline__ void x_update(double (*S)[LP], double (*X)[LP], int* flags, int w, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int rt = 0; rt < PR / 16; rt++) {
+    if (!owns_tile(w, rt)) continue;
+    d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < SB; k += 4)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[16 * rt + lr][C0 + k + lk], S[16 * J + lr][C0 + k + lk], acc, 0, 0, 0);
+#pragma unroll
+    for (int r4 = 0; r4 < 4; r4++) X[16 * rt + lk + 4 * r4][16 * J + lr] -= acc[r4];
+  }
+  lds_signal(&flags[2 * NSUB + J], lane);
+}
+
+template <int C0, int J>
+__device__ __forceinline__ void x_update_far(double (*S)[LP], double (*X)[LP], int* flags, int w, int lane) {
+  if constexpr (J < NSUB) {
+    x_update<C0, J>(S, X, flags, w, lane);
+    x_update_far<C0, J + 1>(S, X, flags, w, lane);
+  }
+}
+
 template <int C0>
-__device__ __forceinline__ void row_chain(double (*S)[LP], double (*X)[LP], double (*Lq)[SB][SB + 2], int* flags,
-                                          int w, int lane, int* info) {
+__device__ __forceinline__ void row_chain(double (*S)[LP], double (*X)[LP], const double (*LR)[LP], const double (*P1)[LP],
+                                          double (*Lq)[SB][SB + 2], int* flags, int w, int lane, bool upd, int* info) {
+  static_assert(SB == 16 && PR == 64, "row tiles are 16 x 16 column blocks");
   if constexpr (C0 < PNB) {
-    constexpr int q = C0 / SB, REST = PNB - C0 - SB;
-    if (w == 1) {
+    constexpr int q = C0 / SB;
+    if (w == 3) {
       lds_wait_ge(&flags[q], 1, info);
-      lds_wait_ge(q == 0 ? &flags[3 * NSUB] : &flags[2 * NSUB + q - 1], 3, info);
+      lds_wait_ge(&flags[2 * NSUB + q], 3 * (q + 1), info);
       double x[SB], row0[SB + 2];
 #pragma unroll
       for (int c = 0; c < SB; c++) x[c] = X[lane][C0 + c];
@@ -556,30 +625,20 @@ __device__ __forceinline__ void row_chain(double (*S)[LP], double (*X)[LP], doub
       for (int c = 0; c < SB; c++) X[lane][C0 + c] = x[c];
       lds_signal(&flags[NSUB + q], lane);
       CST(9 + q);
-    } else {
-      if constexpr (PNB - C0 - SB > 16) {
+    } else if constexpr (PNB - C0 - SB > 16) {
+      if (w <= 2) {  // far S tiles of sub-panel q (column blocks q+2..) while wave 3 solves
         lds_wait_ge(&flags[q], 1, info);
+        if constexpr (q == 0) lds_wait_ge(&flags[5 * NSUB], 3, info);
         far_update<C0>(S, flags, w, lane, info);
       }
+    }
+    if constexpr (q + 1 < NSUB) {
+      la_rows<q + 1>(X, LR, P1, flags, w, lane, upd);
       lds_wait_ge(&flags[NSUB + q], 1, info);
+      x_update<C0, q + 1>(S, X, flags, w, lane);      // the next solve waits on this block
+      x_update_far<C0, q + 2>(S, X, flags, w, lane);  // later blocks
     }
-    if constexpr (REST > 0) {
-      const int lr = lane & 15, lk = lane >> 4;
-      for (int rt = w - 1; rt < PR / 16; rt += 3) {
-#pragma unroll
-        for (int tj = 0; tj < REST / 16; tj++) {
-          d4v acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int k = 0; k < SB; k += 4)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[16 * rt + lr][C0 + k + lk], S[C0 + SB + 16 * tj + lr][C0 + k + lk],
-                                                       acc, 0, 0, 0);
-#pragma unroll
-          for (int r4 = 0; r4 < 4; r4++) X[16 * rt + lk + 4 * r4][C0 + SB + 16 * tj + lr] -= acc[r4];
-        }
-      }
-      lds_signal(&flags[2 * NSUB + q], lane);
-    }
-    row_chain<C0 + SB>(S, X, Lq, flags, w, lane, info);
+    row_chain<C0 + SB>(S, X, LR, P1, Lq, flags, w, lane, upd, info);
   }
 }
 
@@ -599,7 +658,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
   if (threadIdx.x < 64) CST(0);
   if (*done) return;
   static_assert(UT == 64 && PR == 64 && PNB % 16 == 0 && 256 % PNB == 0, "tiling");
-  __shared__ double smem[2 * PNB * LP + 2 * PR * LP + NSUB * SB * (SB + 2) + 3 * NSUB];  // >= 2 * UT * LP (update tiles)
+  __shared__ double smem[2 * PNB * LP + 2 * PR * LP + NSUB * SB * (SB + 2) + 3 * NSUB + 1];  // >= 2 * UT * LP (update tiles)
   const int kb = min(PNB, n - k0);
   const int st = k0 + kb;
   const int t = threadIdx.x;
@@ -695,8 +754,8 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
   double(*X)[LP] = reinterpret_cast<double(*)[LP]>(smem + 2 * PNB * LP);   // A21 -> L21 (PR rows)
   double(*LR)[LP] = reinterpret_cast<double(*)[LP]>(smem + (2 * PNB + PR) * LP);  // L_{R,s-1}
   double(*Lq)[SB][SB + 2] = reinterpret_cast<double(*)[SB][SB + 2]>(smem + 2 * (PNB + PR) * LP);
-  int* flags = reinterpret_cast<int*>(smem + 2 * (PNB + PR) * LP + NSUB * SB * (SB + 2));  // 5 NSUB words
-  if (t < 5 * NSUB) flags[t] = 0;
+  int* flags = reinterpret_cast<int*>(smem + 2 * (PNB + PR) * LP + NSUB * SB * (SB + 2));  // 5 NSUB + 1 words
+  if (t < 5 * NSUB + 1) flags[t] = 0;
   const bool upd = k0 > 0;
   const int kp = k0 - PNB;
   const bool carried = (int)blockIdx.x >= P1;
@@ -736,63 +795,29 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
   __syncthreads();
   if (t < 64) CST(1);
   const int w = t >> 6, lane = t & 63, lr = t & 15, lk = (t >> 4) & 3;
-  if (upd) {  // look-ahead update of the diagonal block by panel s-1: A11 -= L_{s,s-1} L_{s,s-1}^T
-    // (matrix cores, v_mfma_f64_16x16x4; operand maps A[l&15][k=l>>4], B[k=l>>4][l&15]; result row
-    // (l>>4)+4r, column l&15): the lower 16x16 tiles u = w, w+4, .. per wave
-    constexpr int CT = PNB / 16, NT = CT * (CT + 1) / 2;
-#pragma unroll
-    for (int uu = 0; uu < NT; uu += 4) {
-      const int u = uu + w;
-      if (u < NT) {
-        int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= u) ti++;
-        const int tj = u - ti * (ti + 1) / 2;
-        double fa[PNB / 4], fb[PNB / 4];  // every operand read issued before the MFMA chain
-#pragma unroll
-        for (int q = 0; q < PNB; q += 4) {
-          fa[q / 4] = P1s[16 * ti + lr][q + lk];
-          fb[q / 4] = P1s[16 * tj + lr][q + lk];
-        }
-        d4v c2[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};  // two interleaved chains
-#pragma unroll
-        for (int q = 0; q < PNB / 4; q++)
-          c2[q & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c2[q & 1], 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int si = 16 * ti + lk + 4 * r, sj = 16 * tj + lr;
-          if (sj <= si) S[si][sj] -= c2[0][r] + c2[1][r];
-        }
-      }
-    }
+  if (upd) {  // look-ahead update of the diagonal block's first column block by panel s-1:
+    // A11[:, 0:16] -= L_{s,s-1} L_{s,s-1}[0:16]^T, tile (w, 0) per wave (the rest: la_far_tiles, off the chain)
+    la_tile(S, P1s, w, 0, lr, lk);
   }
-  __syncthreads();  // diagonal block complete, flags zeroed
+  __syncthreads();  // first column block of the diagonal block complete, flags zeroed
   if (w == 0) {
     CST(2);
     diag_chain<0>(S, Lq, flags, lane, info);  // the serial chain runs ahead on its own wave
     CST(7);
   } else {
-    if (upd) {  // look-ahead update of this block's rows: A21 -= L_{R,s-1} L_{s,s-1}^T (rows split 3 ways)
+    if (upd) {  // the diagonal block's other look-ahead tiles (ti, tj), 1 <= tj <= ti: two per wave
       constexpr int CT = PNB / 16;
-      for (int rt = w - 1; rt < PR / 16; rt += 3) {
-        d4v cx[CT];
+      int u = 0;
 #pragma unroll
-        for (int j = 0; j < CT; j++) cx[j] = d4v{0.0, 0.0, 0.0, 0.0};
+      for (int ti = 1; ti < CT; ti++)
 #pragma unroll
-        for (int q = 0; q < PNB; q += 4) {
-          const double av = LR[16 * rt + lr][q + lk];
-#pragma unroll
-          for (int j = 0; j < CT; j++)
-            cx[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P1s[16 * j + lr][q + lk], cx[j], 0, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < CT; j++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) X[16 * rt + lk + 4 * r][16 * j + lr] -= cx[j][r];
-      }
+        for (int tj = 1; tj <= ti; tj++, u++)
+          if (u % 3 == w - 1) la_tile(S, P1s, ti, tj, lr, lk);
     }
-    lds_signal(&flags[3 * NSUB], lane);
+    lds_signal(&flags[5 * NSUB], lane);
+    la_rows<0>(X, LR, P1s, flags, w, lane, upd);
     if (w == 1) CST(8);
-    row_chain<0>(S, X, Lq, flags, w, lane, info);
+    row_chain<0>(S, X, LR, P1s, Lq, flags, w, lane, upd, info);
   }
   __syncthreads();
   if (w == 0) CST(13);
