@@ -123,13 +123,15 @@ __device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, i
   float w[4], s[9];
   bilin_w(u, v, u11, v11, w);
   bilin_sample<9>(img, W, u11, v11, w, s);
+  // The residual e and cost of the carried sample are carried too: an accepted step's (f, new_cost)
+  // are exactly what the next iteration would recompute from the same sample (bit-identical).
+  // 1.0/r_norm in double then float == IEEE float division (53 >= 2*24+2, innocuous double rounding)
+  float r_norm_inv = 1.0f / sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+  float e0 = s[0] * r_norm_inv - p[0];
+  float e1 = s[1] * r_norm_inv - p[1];
+  float e2 = s[2] * r_norm_inv - p[2];
+  float cost = e0 * e0 + e1 * e1 + e2 * e2;
   for (int i = 0; i < max_iter; i++) {
-    // 1.0/r_norm in double then float == IEEE float division (53 >= 2*24+2, innocuous double rounding)
-    float r_norm_inv = 1.0f / sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
-    const float e0 = s[0] * r_norm_inv - p[0];
-    const float e1 = s[1] * r_norm_inv - p[1];
-    const float e2 = s[2] * r_norm_inv - p[2];
-    const float cost = e0 * e0 + e1 * e1 + e2 * e2;
     float A00 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
     const float A01 = s[3] * s[6] + s[4] * s[7] + s[5] * s[8];
     float A11 = s[6] * s[6] + s[7] * s[7] + s[8] * s[8];
@@ -155,8 +157,12 @@ __device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, i
       v = v_new;
 #pragma unroll
       for (int k = 0; k < 9; k++) s[k] = t[k];
-      lambda = (float)((double)lambda * 0.1);
+      e0 = f0;
+      e1 = f1;
+      e2 = f2;
       conv = new_cost < cost_thresh;
+      cost = new_cost;
+      lambda = (float)((double)lambda * 0.1);
     } else {
       lambda = (float)((double)lambda * 10.0);
       conv = cost < cost_thresh;
