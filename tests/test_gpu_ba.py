@@ -228,3 +228,28 @@ def test_dense_solve_matches_lapack_on_large_graph(n_kf):
     assert dx.shape == ref.shape == ((n_kf - 1) * 7,)
     # fp64 factorisation, fp32 output: relative to the step size
     np.testing.assert_allclose(dx, ref, rtol=0, atol=2e-6 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_ba_medium_graph_vs_fp64_truth(mode):
+    """A 24-keyframe graph (consecutive + retrieval-like loop edges, 5% outlier matches, 80% valid) at
+    48x64: the full device GN loop (pack, linearisation, several panel launches, carried L^-T) against
+    the fp64 truth build of the oracle, 1e-5 on the poses (SURVEY §8c a-note 6)."""
+    from m3s.synthetic import make_graph, two_way
+
+    G = make_graph(n_kf=24, H=48, W=64, seed=5)
+    ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
+    H, W = 48, 64
+    K = G["K"].numpy()
+    Xs = G["Xs"].numpy()
+    if mode == "calib":
+        Xs = O.backproject_constrain(Xs, K, (H, W))
+    Cs = G["Cs"].numpy()
+    sa, sb = SIG[mode]
+    p = O.ba_params(mode, sa, sb, 0.0, 1.5, K=K, height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    T_ref, _, _ = O.gauss_newton_f64(mode, G["Twc0"].numpy().astype(np.float64), Xs.astype(np.float64),
+                                     Cs[..., 0].astype(np.float64), ii, jj, idx, valid[..., 0],
+                                     Q[..., 0].astype(np.float64), p, 10, 1e-8)
+    T, dx = _call(mode, G["Twc0"].numpy(), Xs, Cs, ii, jj, idx, valid, Q, K, H, W)
+    assert np.isfinite(T).all()
+    np.testing.assert_allclose(T, T_ref, atol=1e-5)
