@@ -139,3 +139,73 @@ class Sim3:
 
     def __repr__(self):
         return f"Sim3({self.data})"
+
+
+class SE3:
+    """lietorch-compatible SE3 (data [t(3), q(4) xyzw]) for the reference's trajectory export
+    (``lietorch_utils.py:6-13`` ``as_SE3``, ``evaluate.py``, ``visualization.py``): the Sim(3) group
+    with the scale fixed to 1."""
+
+    embedded_dim = 7
+    manifold_dim = 6
+
+    def __init__(self, data):
+        self.data = data.data if isinstance(data, SE3) else data
+
+    def _sim3(self):
+        return Sim3(torch.cat((self.data, torch.ones_like(self.data[..., :1])), dim=-1))
+
+    @classmethod
+    def _from_sim3(cls, T):
+        return cls(T.data[..., :7])
+
+    @classmethod
+    def Identity(cls, *batch, device=None, dtype=torch.float32):
+        return cls._from_sim3(Sim3.Identity(*batch, device=device, dtype=dtype))
+
+    @property
+    def shape(self):
+        return self.data.shape[:-1]
+
+    @property
+    def device(self):
+        return self.data.device
+
+    @property
+    def dtype(self):
+        return self.data.dtype
+
+    def __getitem__(self, index):
+        return SE3(self.data[index])
+
+    def __len__(self):
+        return self.data.shape[0]
+
+    def clone(self):
+        return SE3(self.data.clone())
+
+    def to(self, *args, **kwargs):
+        return SE3(self.data.to(*args, **kwargs))
+
+    def cpu(self):
+        return SE3(self.data.cpu())
+
+    def inv(self):
+        return SE3._from_sim3(self._sim3().inv())
+
+    def __mul__(self, other):
+        if not isinstance(other, SE3):
+            return NotImplemented
+        return SE3._from_sim3(self._sim3() * other._sim3())
+
+    def act(self, p):
+        return self._sim3().act(p)
+
+    def translation(self):
+        return self.data[..., :3]
+
+    def matrix(self):
+        return self._sim3().matrix()
+
+    def __repr__(self):
+        return f"SE3({self.data})"

@@ -163,3 +163,25 @@ def test_synthetic_pair_is_consistent():
     D = P["D"]
     np.testing.assert_allclose(D.norm(dim=-1).numpy(), 1.0, atol=1e-5)
     assert (P["Q"] > 1.0).all() and (P["C"] > 1.0).all()
+
+
+def test_se3_is_sim3_with_unit_scale_and_as_se3_pattern():
+    """lietorch_utils.py:6-13 (as_SE3) against the package's lietorch: SE3 from a Sim3's t, q."""
+    import lietorch
+    import torch
+
+    g = torch.Generator().manual_seed(0)
+    q = torch.randn(5, 4, generator=g, dtype=torch.float64)
+    q = q / q.norm(dim=-1, keepdim=True)
+    t = torch.randn(5, 3, generator=g, dtype=torch.float64)
+    s = torch.ones(5, 1, dtype=torch.float64)
+    T = lietorch.Sim3(torch.cat((t, q, s), -1))
+    t_, q_, _ = T.data.split([3, 4, 1], -1)
+    E = lietorch.SE3(torch.cat([t_, q_], dim=-1))
+    p = torch.randn(5, 3, generator=g, dtype=torch.float64)
+    assert isinstance(E, lietorch.SE3)
+    torch.testing.assert_close(E.act(p), T.act(p))
+    torch.testing.assert_close((E * E.inv()).data, lietorch.SE3.Identity(5, dtype=torch.float64).data,
+                               atol=1e-12, rtol=0)
+    torch.testing.assert_close(E.matrix(), T.matrix())
+    assert lietorch.Sim3.embedded_dim == 8 and lietorch.SE3.embedded_dim == 7
