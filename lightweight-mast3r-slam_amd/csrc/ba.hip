@@ -412,6 +412,17 @@ __device__ __forceinline__ void trsm_pipe(double (&x)[W], const double (*Ls)[W +
 }
 
 constexpr int LP = PNB + 2;   // LDS row pitch (doubles) of the panel arrays
+
+// Factorisation results are stored write-through (agent-scope sc1 stores): the next launch reads them
+// on other XCDs anyway, and a launch that left ~28 MB of dirty trailing-matrix lines in L2 paid their
+// write-back at its end (the kernel boundary), on the critical path.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+#ifdef M3S_CHOL_PLAIN_STORES
+  *p = v;
+#else
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
 constexpr int PR = 64;        // rows per panel block
 constexpr int RS = 256 / PNB;  // rows covered by one pass of the block's 256 loading lanes
 
@@ -744,7 +755,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
         for (int r = 0; r < 4; r++) {
           const int i = 32 * wy + 16 * x + lk + 4 * r, j = 32 * wx + 16 * y + lr;
           if (i < nr && j < nc && !(r0 + i < n && c0 + j > r0 + i))  // strictly-upper part unused
-            H[(size_t)(r0 + i) * n + c0 + j] = cold[x][y][r] - acc[x][y][r];
+            st_wt(&H[(size_t)(r0 + i) * n + c0 + j], cold[x][y][r] - acc[x][y][r]);
         }
     return;
   }
@@ -826,7 +837,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* __restrict__ H, 
 #pragma unroll
     for (int q = 0; q < QX; q++) {
       const int i = rs + RS * q, rw = rbase + i;
-      if (rw <= rlim && col < kb) H[(size_t)rw * n + k0 + col] = X[i][col];
+      if (rw <= rlim && col < kb) st_wt(&H[(size_t)rw * n + k0 + col], X[i][col]);
     }
   }
 #ifdef M3S_CHOL_STAMPS
