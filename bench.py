@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the measured HBM-copy / FMA peak probes")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP-event spans inside the timed loop (no roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -101,10 +102,16 @@ def bench_tracking(args, rank, world, dev):
     for i in range(args.warmup):
         step(i)
     iters = []
+    step_s = []
     sync_all(world)
     t0 = time.perf_counter()
+    tp = t0
     for i in range(args.steps):
         new_kf, _, reloc = step(args.warmup + i)
+        # track() returns after its one host readback, so host stamps bracket each frame's device work
+        tn = time.perf_counter()
+        step_s.append(tn - tp)
+        tp = tn
         iters.append(tracker.last_result.iters)
         assert not reloc, "synthetic tracking failed"
     sync_all(world)
@@ -126,7 +133,7 @@ def bench_tracking(args, rank, world, dev):
             kern[name] = (ms.value, cnt.value)
         lib.m3s_timing_reset()
     elapsed = max_over_ranks(elapsed, world)
-    return elapsed, kern, float(np.mean(iters)), H * W
+    return elapsed, kern, float(np.mean(iters)), H * W, step_s
 
 
 def roofline(kern, N, gn_iters_mean):
@@ -206,6 +213,52 @@ def bench_ba(args, rank, world, dev):
             "scaling": "strong", "mode": "rays"}
 
 
+def measured_peaks(dev):
+    """re-measure the peaks on the box — a STREAM-like device copy (torch, 2 x 2 GiB) and a
+    v_fma_f32 loop (libm3s peak probe, 4 waves per SIMD on every CU)."""
+    from m3s import _lib
+
+    lib = _lib.load()
+    n = 1 << 29  # 2 GiB of fp32
+    a = torch.empty(n, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    hbm = 2 * 4 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    out = torch.empty(256, dtype=torch.float32, device=dev)
+    blocks, it = 256 * 16, 4096
+    stream = _lib.stream_ptr(dev)
+    _lib.check(lib.m3s_peak_fma_f32(out.data_ptr(), blocks, it, stream))
+    e0.record()
+    _lib.check(lib.m3s_peak_fma_f32(out.data_ptr(), blocks, it, stream))
+    e1.record()
+    e1.synchronize()
+    fma = blocks * 256 * it * 8 * 2 / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    return {"hbm_copy_GBps": hbm, "fp32_fma_TFLOPs": fma,
+            "how": "torch device copy of 2 GiB (read + write bytes) x10; libm3s v_fma_f32 loop, 4096 blocks x 256"}
+
+
+def frame_roofline(step_s, N, gn_iters_mean, mode):
+    """BASELINE.md §3 per tracked frame: bytes = N (233 + 16 + 29 it), flops = N (11760 + 1700 + c it) with
+    c = 510 (rays) / 380 (calib); fraction = max(bytes / 8 TB/s, flops / 157.3 TFLOP/s) / t_frame (median)."""
+    med = float(np.median(step_s))
+    it = gn_iters_mean
+    byts = N * (233 + 16 + 29 * it)
+    flops = N * (11760 + 1700 + (380 if mode == "calib" else 510) * it)
+    t_b, t_f = byts / (HBM_PEAK_GBS * 1e9), flops / (VALU_F32_PEAK_TFLOPS * 1e12)
+    return {"median_ms": med * 1e3, "p90_ms": float(np.percentile(step_s, 90)) * 1e3, "bytes": byts,
+            "flops": flops, "bound": "hbm" if t_b > t_f else "valu", "frac": max(t_b, t_f) / med,
+            "note": "host-stamped per-frame wall (track() returns after its readback), ViT excluded"}
+
+
 def cpu_baseline(args):
     """Oracle (C restatement + numpy glue) on the host cores, bounded sample of the same workload."""
     import oracle.oracle as O
@@ -263,7 +316,7 @@ def main():
             dist.init_process_group(backend)
     import __graft_entry__  # noqa: F401  (sys.path)
 
-    elapsed, kern, gn_iters, N = bench_tracking(args, rank, world, dev)
+    elapsed, kern, gn_iters, N, step_s = bench_tracking(args, rank, world, dev)
     total_frames = args.steps * world
     value = total_frames / elapsed
     rl = roofline(kern, N, gn_iters)
@@ -280,6 +333,8 @@ def main():
         roof["traffic"] = pmc_traffic(name)
         roof["avg_us"] = d["avg_us"]
         roof["timing"] = "HIP events on the launch stream, second pass of the same K steps"
+    frame = frame_roofline(step_s, N, gn_iters, args.mode)
+    peaks = measured_peaks(dev) if (rank == 0 and not args.no_peaks) else None
     ba = None
     if not args.no_ba:
         ba = bench_ba(args, rank, world, dev)
@@ -299,7 +354,7 @@ def main():
                        "parallelism": f"replicas x{world} (tracking does not shard)",
                        "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
-            "roofline": roof, "cpu_baseline": cpu, "ba": ba,
+            "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

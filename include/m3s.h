@@ -176,6 +176,10 @@ int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s
               int first_chunk, float* T_out_dev /* (16) nullable: T_WCf | T_CkCf on device */,
               m3s_track_result* result /* host */, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Measured-peak probe (no reference counterpart; bench.py's roofline context):
+ * blocks x 256 lanes x iters x 8 chains of v_fma_f32 (2 flops each) on `stream`. */
+int m3s_peak_fma_f32(float* out_dev, int blocks, int iters, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

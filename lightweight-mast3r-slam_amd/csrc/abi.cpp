@@ -33,6 +33,7 @@ hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, i
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
+hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
 }
 
 namespace {
@@ -637,5 +638,14 @@ extern "C" int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const floa
     if ((rc = m3s_ba_solve(&plan, stream)) != M3S_OK) return rc;
   }
   if (iters_out) return m3s_ba_iterations(&plan, iters_out, stream);
+  return M3S_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// measured peak (bench roofline context only)
+// ------------------------------------------------------------------------------------------
+extern "C" int m3s_peak_fma_f32(float* out_dev, int blocks, int iters, void* stream) {
+  M3S_CHECK(out_dev && blocks > 0 && iters > 0, "peak: bad argument");
+  HIP_TRY(m3s_launch_peak_fma_f32(out_dev, blocks, iters, (hipStream_t)stream), "peak launch");
   return M3S_OK;
 }

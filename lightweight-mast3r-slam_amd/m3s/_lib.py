@@ -77,6 +77,7 @@ _SIGS = {
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_iterations": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), c_void_p], c_int),
+    "m3s_peak_fma_f32": ([c_void_p, c_int, c_int, c_void_p], c_int),
     "m3s_match_workspace_size": ([c_int] * 4, c_size_t),
     "m3s_match": ([c_void_p] * 7 + [c_int] * 5 + [c_float] * 3 + [c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
     "m3s_track_workspace_size": ([c_int], c_size_t),
