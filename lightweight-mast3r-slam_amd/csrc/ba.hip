@@ -291,12 +291,23 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
       // M stored upper: index of (min,max)
       const int lo = min(rr, cc), hi = max(rr, cc);
       const int li = lo * 7 - lo * (lo - 1) / 2 + (hi - lo);
+      // contributions summed in CSR order (deterministic); indices and values of 4 at a time in flight
       double s = 0.0;
-      for (int k = a.blk_ptr[b]; k < a.blk_ptr[b + 1]; k++) {
+      const int kb = a.blk_ptr[b], ke = a.blk_ptr[b + 1];
+      int k = kb;
+      for (; k + 4 <= ke; k += 4) {
+        int ent[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) ent[u] = a.blk_ent[k + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = a.edge_sums[(size_t)(ent[u] >> 1) * BA_NSUM + li];
+#pragma unroll
+        for (int u = 0; u < 4; u++) s += ((ent[u] & 1) ? -1.0 : 1.0) * v[u];
+      }
+      for (; k < ke; k++) {
         const int ent = a.blk_ent[k];
-        const int e = ent >> 1;
-        const double sign = (ent & 1) ? -1.0 : 1.0;
-        s += sign * a.edge_sums[(size_t)e * BA_NSUM + li];
+        s += ((ent & 1) ? -1.0 : 1.0) * a.edge_sums[(size_t)(ent >> 1) * BA_NSUM + li];
       }
       a.H[(size_t)(r * 7 + rr) * n + c * 7 + cc] = s;
     }
@@ -304,11 +315,21 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int n, int nb
     const int row = b - nblocks;  // rhs block row
     if (t < 7) {
       double s = 0.0;
-      for (int k = a.rhs_ptr[row]; k < a.rhs_ptr[row + 1]; k++) {
+      const int kb = a.rhs_ptr[row], ke = a.rhs_ptr[row + 1];
+      int k = kb;
+      for (; k + 4 <= ke; k += 4) {
+        int ent[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) ent[u] = a.rhs_ent[k + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = a.edge_sums[(size_t)(ent[u] >> 1) * BA_NSUM + 28 + t];
+#pragma unroll
+        for (int u = 0; u < 4; u++) s += ((ent[u] & 1) ? -1.0 : 1.0) * v[u];
+      }
+      for (; k < ke; k++) {
         const int ent = a.rhs_ent[k];
-        const int e = ent >> 1;
-        const double sign = (ent & 1) ? -1.0 : 1.0;
-        s += sign * a.edge_sums[(size_t)e * BA_NSUM + 28 + t];
+        s += ((ent & 1) ? -1.0 : 1.0) * a.edge_sums[(size_t)(ent >> 1) * BA_NSUM + 28 + t];
       }
       a.H[(size_t)n * n + row * 7 + t] = s;
     }
@@ -857,8 +878,16 @@ __global__ void __launch_bounds__(256) chol_apply_kernel(const double* __restric
   if (i >= n) return;
   const double* c = H + (size_t)(n + 1 + i) * n;
   const double* y = H + (size_t)n * n;
-  double s = 0.0;
-  for (int j = (i & ~63) + lane; j < n; j += 64) s += j >= i ? c[j] * y[j] : 0.0;
+  double s0 = 0.0, s1 = 0.0;  // two interleaved partial sums, four row loads per lane in flight
+  int j = (i & ~63) + lane;
+  for (; j + 192 < n; j += 256) {
+    const double c0 = c[j], c1 = c[j + 64], c2 = c[j + 128], c3 = c[j + 192];
+    const double y0 = y[j], y1 = y[j + 64], y2 = y[j + 128], y3 = y[j + 192];
+    s0 += (j >= i ? c0 * y0 : 0.0) + (j + 128 >= i ? c2 * y2 : 0.0);
+    s1 += (j + 64 >= i ? c1 * y1 : 0.0) + (j + 192 >= i ? c3 * y3 : 0.0);
+  }
+  for (; j < n; j += 64) s0 += j >= i ? c[j] * y[j] : 0.0;
+  double s = s0 + s1;
   s = wave_sum(s);
   if (lane == 0) x[i] = s;
 }
