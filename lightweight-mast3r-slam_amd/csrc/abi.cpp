@@ -277,8 +277,11 @@ static TrackState* pinned_state() {
 
 static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
 
-static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, double** partials, float** rec) {
+static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, double** partials, float** rec,
+                          unsigned long long** cnt, unsigned** tick) {
   *st = c.take<TrackState>(1);
+  *cnt = c.take<unsigned long long>(M3S_TRACK_SHARDS * 16);
+  *tick = c.take<unsigned>((M3S_TRACK_SHARDS + 1) * 32);
   *flags = c.take<uint8_t>(((size_t)N + 15) / 16 * 16);
   *partials = c.take<double>((size_t)track_nparts(N) * 40);
   *rec = c.take<float>((size_t)N * 8);
@@ -291,7 +294,9 @@ extern "C" size_t m3s_track_workspace_size(int N) {
   uint8_t* bm;
   double* pa;
   float* rec;
-  return track_carve(c, N, &st, &bm, &pa, &rec);
+  unsigned long long* cnt;
+  unsigned* tick;
+  return track_carve(c, N, &st, &bm, &pa, &rec, &cnt, &tick);
 }
 
 extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s_track_fuse_args* fuse,
@@ -316,7 +321,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   Carver c(workspace);
   TrackArgs a;
   TrackState* st;
-  track_carve(c, N, &st, &a.flags, &a.partials, &a.rec);
+  track_carve(c, N, &st, &a.flags, &a.partials, &a.rec, &a.cnt, &a.tick);
   a.state = st;
   a.idx = in->idx_f2k;
   a.valid_match = in->valid_match;

@@ -8,6 +8,8 @@
 #define M3S_TRACK_CHOLESKY_FAILED 3
 #define M3S_TRACK_SKIPPED 4
 
+#define M3S_TRACK_SHARDS 8  // counter shards (one per XCD: blocks are dealt to XCDs round-robin)
+
 // Device-resident GN state (one per tracked frame). Layout mirrored by m3s/_track.py (M3S_TRACK_STATE_*).
 struct TrackState {
   float T[8];      // T_CkCf (current estimate)
@@ -21,7 +23,6 @@ struct TrackState {
   int n_valid_opt;
   int n_valid_kf;
   int n_unique;
-  int arrive;      // per-iteration block-arrival ticket of the fused GN kernel (last arriver solves)
   int done_chunk;  // host chunk id of the GN launch batch that finished (gates the fuse launch)
 };
 
@@ -53,6 +54,8 @@ struct TrackArgs {
   uint8_t* flags;              // (N, padded to 16) unique(idx[valid]) byte map (workspace, zeroed per frame)
   double* partials;            // (nparts, 40) block partial sums (workspace)
   TrackState* state;
+  unsigned long long* cnt;     // (8 x 16) setup counters, one 128-B line per XCD shard: (n_valid_kf << 32) | n_valid_opt
+  unsigned* tick;              // (9 x 32) GN arrival tickets: 8 shards + the top counter, one 128-B line each
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
 };
 

@@ -64,9 +64,11 @@ __device__ __forceinline__ void sim3_inv(const float* A, float* C) {
 // state <- {0, T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}; the grid zeroes
 // the unique-idx byte map (replaces two memsets + a one-lane launch)
 __global__ void __launch_bounds__(256) track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk,
-                                                         uint4* flags, int n16) {
+                                                         uint4* flags, int n16, unsigned long long* cnt, unsigned* tick) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) flags[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i < M3S_TRACK_SHARDS * 16) cnt[i] = 0ull;
+  for (int j = i; j < (M3S_TRACK_SHARDS + 1) * 32; j += gridDim.x * blockDim.x) tick[j] = 0u;
   if (i != 0) return;
   *st = TrackState{};
   float Ti[8], Tf[8], Tk[8];
@@ -136,23 +138,29 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
       rec[1] = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
     }
   }
-  // block-reduce the two counters, one atomic per block
-  __shared__ int s_cnt[2][4];
+  // block-reduce the two counters into one packed 64-bit add on this block's XCD shard: one counter word
+  // for all 1024 blocks serialises the adds (~11 ns each, MI355X_MICROARCH.md "fanin")
+  __shared__ unsigned long long s_cnt[4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long bo = __ballot(v_opt), bk = __ballot(v_kf);
-  if (lane == 0) {
-    s_cnt[0][wid] = __popcll(bo);
-    s_cnt[1][wid] = __popcll(bk);
-  }
+  const unsigned long long bo = __ballot(v_opt), bk = __ballot(v_kf);
+  if (lane == 0) s_cnt[wid] = ((unsigned long long)__popcll(bk) << 32) | (unsigned long long)__popcll(bo);
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(&a.state->n_valid_opt, s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3]);
-    atomicAdd(&a.state->n_valid_kf, s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3]);
+    const unsigned long long v = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (v) atomicAdd(&a.cnt[16 * (blockIdx.x % M3S_TRACK_SHARDS)], v);
   }
 }
 
-__device__ __forceinline__ bool track_skipped(const TrackState* st, const TrackParams& p) {
-  return (float)st->n_valid_opt / (float)p.N < p.min_match_frac;  // tracker.py:67-70
+// the setup counters summed over the shards: low 32 bits n_valid_opt, high 32 bits n_valid_kf
+__device__ __forceinline__ unsigned long long track_counts(const unsigned long long* cnt) {
+  unsigned long long v = 0;
+#pragma unroll
+  for (int s = 0; s < M3S_TRACK_SHARDS; s++) v += cnt[16 * s];
+  return v;
+}
+
+__device__ __forceinline__ bool track_skipped(unsigned n_valid_opt, const TrackParams& p) {
+  return (float)n_valid_opt / (float)p.N < p.min_match_frac;  // tracker.py:67-70
 }
 
 // accumulate one whitened row (tracker.py:156-166): robust = si*sqrt(huber(si*r)); A = robust*J; b = robust*r
@@ -289,6 +297,7 @@ __device__ unsigned long long g_gn_stamps[8 * 16];
 
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) int gint;
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 #define GN_THREADS 256
 #define GN_PPT 4     // points per thread per round: all their record loads issued before any math
@@ -381,7 +390,12 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
 __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackParams p, int chunk_id) {
   TrackState* st = a.state;
   if (st->done) return;
-  if (track_skipped(st, p)) {
+  const unsigned long long counts = track_counts(a.cnt);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the host readback (same values every launch)
+    st->n_valid_opt = (int)(unsigned)counts;
+    st->n_valid_kf = (int)(unsigned)(counts >> 32);
+  }
+  if (track_skipped((unsigned)counts, p)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       st->status = M3S_TRACK_SKIPPED;
       st->done = 1;
@@ -427,9 +441,15 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
                        __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add((gint*)&st->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == (int)gridDim.x - 1);
+  if (threadIdx.x == 0) {  // two-level ticket: this block's XCD shard, then the top counter by each shard's last
+    const unsigned sh = blockIdx.x % M3S_TRACK_SHARDS;
+    const unsigned nsh = min(gridDim.x, (unsigned)M3S_TRACK_SHARDS);
+    const unsigned per = (gridDim.x - sh + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;
+    bool last = false;
+    if (__hip_atomic_fetch_add((gu32*)&a.tick[32 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1)
+      last = __hip_atomic_fetch_add((gu32*)&a.tick[32 * M3S_TRACK_SHARDS], 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return;
@@ -458,8 +478,9 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
 #ifdef M3S_GN_STAMPS
     if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
-    __hip_atomic_store((gint*)&st->arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   }
+  if (threadIdx.x <= M3S_TRACK_SHARDS)  // every block has arrived: re-arm the tickets for the next launch
+    __hip_atomic_store((gu32*)&a.tick[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77). Runs only if the
@@ -518,7 +539,7 @@ extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_W
                                             hipStream_t s) {
   const int n16 = (N + 15) / 16;  // the byte map is carved with a 16-B padded length
   hipLaunchKernelGGL(m3s::track_init_kernel, dim3((n16 + 255) / 256), dim3(256), 0, s, a->state, T_WCf, T_WCk,
-                     reinterpret_cast<uint4*>(a->flags), n16);
+                     reinterpret_cast<uint4*>(a->flags), n16, a->cnt, a->tick);
   return hipGetLastError();
 }
 
