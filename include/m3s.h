@@ -176,6 +176,21 @@ int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s
               int first_chunk, float* T_out_dev /* (16) nullable: T_WCf | T_CkCf on device */,
               m3s_track_result* result /* host */, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- retrieval codebook quantization ----
+ * Replaces RetrievalDatabase.quantize_custom (mast3r_slam/retrieval_database.py:96-105):
+ *   l2 = (|q|^2 + |c|^2) - 2 q c^T ; topk(l2, k, largest=False).indices, called from accumulate_scores (:119)
+ *   and add_to_ivf_custom (:151-153) with the codebook `self.centroids` (:20-22).
+ * m3s_codebook_prepare arranges the (C, D) fp32 centroids once (the reference moves them to the device once, in
+ * __init__) into `codebook` (m3s_codebook_size bytes, device). m3s_quantize writes the (M, k) int64 indices of the
+ * k nearest centroids of each of the M query rows (ascending distance; ties -> lower index), 1 <= k <= 8, k <= C.
+ * Distances are computed with bf16 hi/lo split products on the matrix cores (fp32 accumulation): ~2^-16 relative
+ * per product, tighter than the reference's TF32 GEMM (main.py:168). Everything is asynchronous on `stream`. */
+size_t m3s_codebook_size(int C, int D);
+int m3s_codebook_prepare(const float* centroids, int C, int D, void* codebook, size_t codebook_bytes, void* stream);
+size_t m3s_quantize_workspace_size(int C, int D, int M, int k);
+int m3s_quantize(const void* codebook, int C, int D, const float* qvecs, int M, int k, int64_t* topk_out,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
 /* Measured-peak probe (no reference counterpart; bench.py's roofline context):
  * blocks x 256 lanes x iters x 8 chains of v_fma_f32 (2 flops each) on `stream`. */
 int m3s_peak_fma_f32(float* out_dev, int blocks, int iters, void* stream);

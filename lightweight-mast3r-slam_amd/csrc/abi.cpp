@@ -34,6 +34,10 @@ hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
+hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, hipStream_t);
+hipError_t m3s_launch_rq_norm(const float*, int, int, int, float, float*, hipStream_t);
+hipError_t m3s_launch_rq_topk(const uint4*, const float*, const uint4*, const float*, int, int, int, int, int,
+                              unsigned long long*, int64_t*, hipStream_t);
 }
 
 namespace {
@@ -652,5 +656,93 @@ extern "C" int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const floa
 extern "C" int m3s_peak_fma_f32(float* out_dev, int blocks, int iters, void* stream) {
   M3S_CHECK(out_dev && blocks > 0 && iters > 0, "peak: bad argument");
   HIP_TRY(m3s_launch_peak_fma_f32(out_dev, blocks, iters, (hipStream_t)stream), "peak launch");
+  return M3S_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// retrieval codebook quantization (retrieval_database.py:96-105; kernels in retrieval.hip)
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int RQ_ROWS = 256, RQ_QG = 304, RQ_NQT = 19;  // retrieval.hip: rows per block, queries per group
+inline int rq_steps(int D) { return (D + 31) / 32; }
+inline int rq_rows_padded(int C) { return (C + RQ_ROWS - 1) / RQ_ROWS * RQ_ROWS; }
+inline int rq_groups(int M) { return (M + RQ_QG - 1) / RQ_QG; }
+
+size_t codebook_carve(Carver& c, int C, int D, uint4** frag, float** cn) {
+  const size_t Cp = (size_t)rq_rows_padded(C);
+  *frag = c.take<uint4>(Cp / 16 * rq_steps(D) * 128);  // (Cp/16 tiles) x S x {hi, lo} x 64 lanes (rq_prep_kernel)
+  *cn = c.take<float>(Cp);
+  return c.off;
+}
+
+size_t quantize_carve(Carver& c, int C, int D, int M, int k, uint4** qfrag, float** qn, unsigned long long** cand) {
+  const int G = rq_groups(M);
+  *qfrag = c.take<uint4>((size_t)G * rq_steps(D) * RQ_NQT * 128);
+  *qn = c.take<float>((size_t)G * RQ_QG);
+  *cand = c.take<unsigned long long>((size_t)G * (rq_rows_padded(C) / RQ_ROWS) * RQ_QG * k);
+  return c.off;
+}
+}  // namespace
+
+extern "C" size_t m3s_codebook_size(int C, int D) {
+  if (C <= 0 || D <= 0) return 0;
+  Carver c(nullptr);
+  uint4* f;
+  float* n;
+  return codebook_carve(c, C, D, &f, &n);
+}
+
+extern "C" int m3s_codebook_prepare(const float* centroids, int C, int D, void* codebook, size_t codebook_bytes,
+                                    void* stream) {
+  M3S_CHECK(centroids && codebook, "codebook: null argument");
+  M3S_CHECK(C > 0 && D > 0, "codebook: C and D must be positive");
+  M3S_CHECK((long long)rq_rows_padded(C) * rq_steps(D) * 32 < (1ll << 31), "codebook: too large");
+  if (codebook_bytes < m3s_codebook_size(C, D)) return fail(M3S_ESPACE, "codebook: buffer too small");
+  Carver c(codebook);
+  uint4* frag;
+  float* cn;
+  codebook_carve(c, C, D, &frag, &cn);
+  hipStream_t s = (hipStream_t)stream;
+  const int Cp = rq_rows_padded(C);
+  HIP_TRY(m3s_launch_rq_prep(centroids, C, D, rq_steps(D), Cp / 16, RQ_ROWS / 16, frag, s), "codebook prep launch");
+  HIP_TRY(m3s_launch_rq_norm(centroids, C, D, Cp, __builtin_inff(), cn, s), "codebook norm launch");
+  return M3S_OK;
+}
+
+extern "C" size_t m3s_quantize_workspace_size(int C, int D, int M, int k) {
+  if (C <= 0 || D <= 0 || M <= 0 || k <= 0) return 0;
+  Carver c(nullptr);
+  uint4* q;
+  float* n;
+  unsigned long long* cand;
+  return quantize_carve(c, C, D, M, k, &q, &n, &cand);
+}
+
+extern "C" int m3s_quantize(const void* codebook, int C, int D, const float* qvecs, int M, int k, int64_t* topk_out,
+                            void* workspace, size_t workspace_bytes, void* stream) {
+  M3S_CHECK(codebook && qvecs && topk_out && workspace, "quantize: null argument");
+  M3S_CHECK(C > 0 && D > 0 && M > 0, "quantize: C, D and M must be positive");
+  M3S_CHECK(k >= 1 && k <= 8, "quantize: k (multiple_assignment) must be in 1..8");
+  M3S_CHECK(k <= C, "quantize: k larger than the codebook (torch.topk: selected index k out of range)");
+  M3S_CHECK(rq_groups(M) < 65536, "quantize: too many query rows");
+  if (workspace_bytes < m3s_quantize_workspace_size(C, D, M, k)) return fail(M3S_ESPACE, "quantize: workspace too small");
+  Carver cb(const_cast<void*>(codebook));
+  uint4* cfrag;
+  float* cn;
+  codebook_carve(cb, C, D, &cfrag, &cn);
+  Carver c(workspace);
+  uint4* qfrag;
+  float* qn;
+  unsigned long long* cand;
+  quantize_carve(c, C, D, M, k, &qfrag, &qn, &cand);
+  hipStream_t s = (hipStream_t)stream;
+  const int G = rq_groups(M), S = rq_steps(D);
+  HIP_TRY(m3s_launch_rq_prep(qvecs, M, D, S, G * RQ_NQT, RQ_NQT, qfrag, s), "quantize prep launch");
+  HIP_TRY(m3s_launch_rq_norm(qvecs, M, D, G * RQ_QG, 0.0f, qn, s), "quantize norm launch");
+  {
+    Span sp("quantize_topk", s);
+    HIP_TRY(m3s_launch_rq_topk(cfrag, cn, qfrag, qn, S, rq_rows_padded(C) / RQ_ROWS, G, M, k, cand, topk_out, s),
+            "quantize topk launch");
+  }
   return M3S_OK;
 }

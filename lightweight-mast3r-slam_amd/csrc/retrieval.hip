@@ -1,0 +1,421 @@
+// Retrieval codebook quantization for MI355X (gfx950): the distance GEMM + top-k of
+// RetrievalDatabase.quantize_custom (/root/reference/mast3r_slam/retrieval_database.py:96-105):
+//
+//   l2[m, c] = (|q_m|^2 + |c_c|^2) - 2 q_m . c_c        (fp32, torch broadcasting order)
+//   topk(l2, k, dim=1, largest=False).indices           (ascending distance, int64)
+//
+// At the reference's shapes (asmk codebook 64k x 1024, 300 local features per keyframe, k = 5 for a
+// query, 1 for a database add: mast3r/retrieval/processor.py:91-97, model.py:108-109) this is a
+// 300 x 65536 x 1024 GEMM whose 256 MB codebook is streamed once per call. The reference runs it as a
+// TF32 GEMM (main.py:168 enables TF32 matmuls) followed by torch.topk.
+//
+// MI355X design:
+//   * Matrix cores in bf16 with a hi/lo split: x = hi + lo (both bf16, |lo| <= 2^-9 |x|) and
+//     q.c ~= qh.ch + qh.cl + ql.ch, fp32 accumulation (v_mfma_f32_16x16x32_bf16). Per-product error
+//     ~2^-16 relative: ~100x tighter than the reference's own TF32 product (10-bit mantissas), at
+//     3 MFMA per product = 3 x 2.5 PF/s dense bf16 instead of the 157 TF/s fp32 MFMA rate.
+//   * Both operands are pre-arranged in MFMA fragment order (one 16-B unit per lane per 16x32
+//     tile): the codebook once (m3s_codebook_prepare), the queries per call. A k-step's operands are
+//     then contiguous, staged by lane-linear global_load_lds copies, and read back conflict-free.
+//   * One 512-thread block per 256 codebook rows (256 blocks = one per CU at 64k rows), two waves
+//     per SIMD: wave w owns 32 rows (two 16-row tiles) against all 19 query tiles of the group, i.e.
+//     38 16x16 fp32 accumulator tiles = 152 registers per lane (no spills at 256 per wave).
+//     Codebook (32 KB) and query (38 KB) k-step images are double-buffered in LDS; each query
+//     fragment pair read feeds 6 MFMAs, each codebook fragment pair 57.
+//   * Epilogue (exact block top-k per query, keys = order-preserving fp32 bits << 32 | row): a
+//     query's 256 block distances sit in 32 lanes, 8 each. tau = the k-th smallest of the 32 lane
+//     minima bounds the k-th best, so only distances <= tau (typically ~6 per query and block) are
+//     appended to LDS lists and sorted. rq_merge_kernel reduces the blocks' keys (one wave per
+//     query) and writes the indices. Ties break to the lower codebook row (torch.topk leaves them
+//     unspecified).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace m3s {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const void* rq_gptr;
+typedef __attribute__((address_space(3))) void* rq_lptr;
+
+#define RQ_NQT 19                 // query column tiles (16 queries) per group
+#define RQ_QG (RQ_NQT * 16)       // 304 queries per group
+#define RQ_NR 2                   // codebook row tiles (16 rows) per wave
+#define RQ_ROWS 256               // codebook rows per block: 8 waves x 32
+#define RQ_THREADS 512            // 8 waves
+#define RQ_NL 32                  // lane slots per query in a block: 8 waves x 4 lane groups
+#define RQ_BT (RQ_ROWS / 16)      // codebook row tiles per block
+#define RQ_QU (RQ_NQT * 2 * 64)   // 16-B query units per (group, k-step): 19 tiles x {hi, lo} x 64 lanes
+#define RQ_AU (RQ_BT * 2 * 64)    // 16-B codebook units per (block, k-step): 16 tiles x {hi, lo} x 64 lanes
+#define RQ_CAP 24                 // epilogue candidate list length per query
+
+__device__ __forceinline__ unsigned bf16_rne_bits(float x) {
+  unsigned u = __float_as_uint(x);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+// Split 8 consecutive fp32 values into bf16 hi / lo fragments (8 x bf16 each, packed in a uint4).
+__device__ __forceinline__ void split8(const float (&v)[8], uint4& hi, uint4& lo) {
+  unsigned h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    h[j] = bf16_rne_bits(v[j]);
+    l[j] = bf16_rne_bits(v[j] - __uint_as_float(h[j] << 16));
+  }
+  hi = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+  lo = make_uint4(l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16));
+}
+
+// Fragment layout: tile T (16 rows) of k-step s, part p (hi/lo), lane l holds rows 16T + (l & 15),
+// columns 32s + 8(l >> 4) .. +7. Unit index (((T / inner_n) * S + s) * inner_n + T % inner_n) * 2 + p)
+// * 64 + l: inner_n = RQ_BT for the codebook (a block's k-step contiguous, 32 KB), RQ_NQT for the
+// queries (a group's k-step contiguous, 38 KB). Rows >= R and columns >= D are zero.
+__global__ void __launch_bounds__(256) rq_prep_kernel(const float* __restrict__ X, int R, int D, int S, int ntiles,
+                                                      int inner_n, uint4* __restrict__ frag) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)ntiles * S * 64;
+  if (gid >= total) return;
+  const int lane = (int)(gid & 63);
+  const size_t ts = gid >> 6;
+  const int s = (int)(ts % S);
+  const int T = (int)(ts / S);
+  const int row = 16 * T + (lane & 15), k0 = 32 * s + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) v[j] = (row < R && k0 + j < D) ? X[(size_t)row * D + k0 + j] : 0.0f;
+  uint4 hi, lo;
+  split8(v, hi, lo);
+  const size_t u = ((((size_t)(T / inner_n) * S + s) * inner_n + T % inner_n) * 2) * 64 + lane;
+  frag[u] = hi;
+  frag[u + 64] = lo;
+}
+
+// |x_r|^2 in fp32 (one wave per row); rows in [R, Rp) get pad_value (+inf for the codebook, so
+// padded rows never rank; 0 for padded queries, whose results are not written).
+__global__ void __launch_bounds__(256) rq_norm_kernel(const float* __restrict__ X, int R, int D, int Rp, float pad_value,
+                                                      float* __restrict__ nrm) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= Rp) return;
+  float s = 0.0f;
+  if (row < R)
+    for (int k = lane; k < D; k += 64) {
+      const float x = X[(size_t)row * D + k];
+      s += x * x;
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) nrm[row] = row < R ? s : pad_value;
+}
+
+__device__ __forceinline__ unsigned long long dist_key(float d, unsigned row) {
+  unsigned u = __float_as_uint(d);
+  u ^= (u & 0x80000000u) ? 0xffffffffu : 0x80000000u;  // order-preserving fp32 -> u32
+  return ((unsigned long long)u << 32) | row;
+}
+
+// insert key into the ascending list L (keeps the K smallest)
+template <int K>
+__device__ __forceinline__ void kins(unsigned long long (&L)[K], unsigned long long key) {
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    const unsigned long long o = L[j];
+    const bool lt = key < o;
+    L[j] = lt ? key : o;
+    key = lt ? o : key;
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void kmerge_xor(unsigned long long (&L)[K], int off) {
+  unsigned long long P[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) P[j] = __shfl_xor(L[j], off, 64);
+#pragma unroll
+  for (int j = 0; j < K; j++) kins<K>(L, P[j]);
+}
+
+// grid (Cp / 256, groups); block 512. cand[((g * nblk + b) * RQ_QG + q) * K + j]: the block's K best keys.
+template <int K>
+__global__ void __launch_bounds__(RQ_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ cn, const uint4* __restrict__ qfrag,
+                    const float* __restrict__ qn, int S, unsigned long long* __restrict__ cand) {
+  __shared__ uint4 sb_[2][RQ_QU];  // query k-step images
+  __shared__ uint4 sa_[2][RQ_AU];  // codebook k-step images
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int g = blockIdx.y;
+  const uint4* ca = cfrag + (size_t)blockIdx.x * S * RQ_AU + lane;
+  const uint4* qa = qfrag + (size_t)g * S * RQ_QU + lane;
+  constexpr int NA = RQ_AU / 64, NCP = NA + RQ_QU / 64;  // 1-KB wave copies per k-step: 32 codebook + 38 query
+  f4v acc[RQ_NR][RQ_NQT];
+#pragma unroll
+  for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+    for (int q = 0; q < RQ_NQT; q++) acc[r][q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  // k-step images: lane-linear 1-KB global_load_lds copies dealt round-robin to the 8 waves
+  auto stage = [&](int s, int b) {
+    for (int i = w; i < NCP; i += RQ_THREADS / 64) {
+      if (i < NA) {
+#ifndef RQ_EXP_NOLOAD  // (experiment builds only) no codebook stream: every k-step reuses step 0's image
+        __builtin_amdgcn_global_load_lds((rq_gptr)(ca + (size_t)s * RQ_AU + i * 64), (rq_lptr)&sa_[b][i * 64], 16, 0, 0);
+#endif
+      } else {
+        __builtin_amdgcn_global_load_lds((rq_gptr)(qa + (size_t)s * RQ_QU + (i - NA) * 64),
+                                         (rq_lptr)&sb_[b][(i - NA) * 64], 16, 0, 0);
+      }
+    }
+  };
+#ifdef RQ_EXP_NOLOAD
+  for (int i = w; i < NA; i += RQ_THREADS / 64) {
+    __builtin_amdgcn_global_load_lds((rq_gptr)(ca + i * 64), (rq_lptr)&sa_[0][i * 64], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((rq_gptr)(ca + i * 64), (rq_lptr)&sa_[1][i * 64], 16, 0, 0);
+  }
+#endif
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < S; s++) {
+    const int buf = s & 1;
+    if (s + 1 < S) stage(s + 1, buf ^ 1);  // in flight behind this step's MFMAs
+    bf16x8 ah[RQ_NR], al[RQ_NR];
+#pragma unroll
+    for (int r = 0; r < RQ_NR; r++) {
+      ah[r] = __builtin_bit_cast(bf16x8, sa_[buf][((w * RQ_NR + r) * 2) * 64 + lane]);
+      al[r] = __builtin_bit_cast(bf16x8, sa_[buf][((w * RQ_NR + r) * 2 + 1) * 64 + lane]);
+    }
+    const uint4* sb = &sb_[buf][lane];
+    uint4 bh = sb[0], bl = sb[64];
+#pragma unroll
+    for (int q = 0; q < RQ_NQT; q++) {
+      uint4 nh = bh, nl = bl;
+      if (q + 1 < RQ_NQT) {  // next tile's fragments in flight behind this tile's 6 MFMAs
+        nh = sb[(2 * q + 2) * 64];
+        nl = sb[(2 * q + 3) * 64];
+      }
+      const bf16x8 vh = __builtin_bit_cast(bf16x8, bh), vl = __builtin_bit_cast(bf16x8, bl);
+#pragma unroll
+      for (int r = 0; r < RQ_NR; r++) acc[r][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], vh, acc[r][q], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < RQ_NR; r++) acc[r][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], vl, acc[r][q], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < RQ_NR; r++) acc[r][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[r], vh, acc[r][q], 0, 0, 0);
+      bh = nh;
+      bl = nl;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k-step s+1 staged (this wave's copies) ...
+    __syncthreads();                                  // ... and every wave's; buffer `buf` no longer read
+  }
+
+  // ---- epilogue: exact block top-K per query by a threshold filter ----
+#ifdef RQ_EXP_NOEPI  // (experiment builds only) skip the top-k: one checksum store per lane
+  {
+    float sum = 0.0f;
+#pragma unroll
+    for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+      for (int q = 0; q < RQ_NQT; q++) sum += acc[r][q][0] + acc[r][q][1] + acc[r][q][2] + acc[r][q][3];
+    if (sum == 12345.0f) cand[t] = 0;
+    return;
+  }
+#endif
+  //   1. every lane takes the minimum of its 8 distances of a query; tau[q] = the K-th smallest of the
+  //      query's 32 lane minima, so at least K distances are <= tau[q] and the K best all are;
+  //   2. every lane appends its distances <= tau[q] to the query's LDS list (one LDS atomic per lane and
+  //      query tile reserves the slots);
+  //   3. one thread per query keeps the K best of the list (the (distance, row) order of a full sort).
+  // A list longer than RQ_CAP (many equal distances, or tau = +inf when fewer than K lanes hold codebook
+  // rows) is redone for its query tile by exhaustive per-lane insertion + merges.
+  const unsigned row0 = blockIdx.x * RQ_ROWS + w * (16 * RQ_NR) + (lane >> 4) * 4;
+  float cv[RQ_NR][4];
+#pragma unroll
+  for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) cv[r][i] = cn[row0 + 16 * r + i];
+  float* smin = reinterpret_cast<float*>(&sb_[0][0]);  // [RQ_QG][RQ_NL] lane minima
+  float* tau = smin + RQ_QG * RQ_NL;                   // [RQ_QG]
+  int* cnt = reinterpret_cast<int*>(tau + RQ_QG);      // [RQ_QG] list lengths
+  int* ovf = cnt + RQ_QG;                              // [32] query-tile overflow flags
+  unsigned long long* lst = reinterpret_cast<unsigned long long*>(&sa_[0][0]);  // [RQ_QG][RQ_CAP]
+  static_assert(4 * (RQ_QG * (RQ_NL + 2) + 32) <= (int)sizeof(sb_), "epilogue scalars fit the query images");
+  static_assert(8 * RQ_QG * RQ_CAP <= (int)sizeof(sa_), "candidate lists fit the codebook images");
+  static_assert(8 * 16 * K <= RQ_QG * RQ_CAP, "fallback lists fit the candidate lists");
+  const int col = lane & 15, lg = w * 4 + (lane >> 4);  // query column in the tile; lane slot of the query
+#pragma unroll 19  // explicit count: a plain full-unroll request is declined for large K (acc -> scratch)
+  for (int q = 0; q < RQ_NQT; q++) {
+    const int ql = 16 * q + col;
+    const float qv = qn[g * RQ_QG + ql];
+    float m = __builtin_inff();
+#pragma unroll
+    for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) m = fminf(m, (qv + cv[r][i]) - 2.0f * acc[r][q][i]);
+    smin[ql * RQ_NL + lg] = m;
+  }
+  __syncthreads();
+  for (int ql = t; ql < RQ_QG; ql += RQ_THREADS) {
+    float L[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) L[j] = __builtin_inff();
+#pragma unroll
+    for (int u = 0; u < RQ_NL; u++) {
+      float v = smin[ql * RQ_NL + u];
+#pragma unroll
+      for (int j = 0; j < K; j++) {  // sorted insertion (values only)
+        const float o = L[j];
+        L[j] = fminf(o, v);
+        v = fmaxf(o, v);
+      }
+    }
+    tau[ql] = L[K - 1];
+    cnt[ql] = 0;
+  }
+  if (t < 32) ovf[t] = 0;
+  __syncthreads();
+#pragma unroll 19  // explicit count: a plain full-unroll request is declined for large K (acc -> scratch)
+  for (int q = 0; q < RQ_NQT; q++) {
+    const int ql = 16 * q + col;
+    const float qv = qn[g * RQ_QG + ql];
+    const float tq = tau[ql];
+    unsigned mask = 0;
+#pragma unroll
+    for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float d = (qv + cv[r][i]) - 2.0f * acc[r][q][i];
+        mask |= (d <= tq && d < __builtin_inff()) ? 1u << (4 * r + i) : 0u;
+      }
+    if (mask) {
+      int slot = atomicAdd(&cnt[ql], __popc(mask));
+#pragma unroll
+      for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (mask & (1u << (4 * r + i))) {
+            if (slot < RQ_CAP)
+              lst[ql * RQ_CAP + slot] = dist_key((qv + cv[r][i]) - 2.0f * acc[r][q][i], row0 + 16 * r + i);
+            slot++;
+          }
+    }
+  }
+  __syncthreads();
+  for (int ql = t; ql < RQ_QG; ql += RQ_THREADS) {
+    const int n = cnt[ql];
+    if (n > RQ_CAP) {
+      ovf[ql >> 4] = 1;
+      continue;
+    }
+    unsigned long long L[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) L[j] = ~0ull;
+    for (int u = 0; u < n; u++) kins<K>(L, lst[ql * RQ_CAP + u]);
+    unsigned long long* o = cand + ((size_t)(g * gridDim.x + blockIdx.x) * RQ_QG + ql) * K;
+#pragma unroll
+    for (int j = 0; j < K; j++) o[j] = L[j];
+  }
+  __syncthreads();
+  unsigned long long* sk = lst;  // fallback merge lists [8 waves][16][K]
+#pragma unroll 19  // explicit count: a plain full-unroll request is declined for large K (acc -> scratch)
+  for (int q = 0; q < RQ_NQT; q++) {
+    if (ovf[q]) {  // block-uniform
+      const float qv = qn[g * RQ_QG + 16 * q + col];
+      unsigned long long L[K];
+#pragma unroll
+      for (int j = 0; j < K; j++) L[j] = ~0ull;
+#pragma unroll
+      for (int r = 0; r < RQ_NR; r++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) kins<K>(L, dist_key((qv + cv[r][i]) - 2.0f * acc[r][q][i], row0 + 16 * r + i));
+      kmerge_xor<K>(L, 16);
+      kmerge_xor<K>(L, 32);
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < K; j++) sk[(w * 16 + lane) * K + j] = L[j];
+      }
+      __syncthreads();
+      if (t < 16 && cnt[16 * q + t] > RQ_CAP) {
+        unsigned long long M[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) M[j] = sk[t * K + j];
+#pragma unroll
+        for (int ww = 1; ww < RQ_THREADS / 64; ww++)
+#pragma unroll
+          for (int j = 0; j < K; j++) kins<K>(M, sk[(ww * 16 + t) * K + j]);
+        unsigned long long* o = cand + ((size_t)(g * gridDim.x + blockIdx.x) * RQ_QG + 16 * q + t) * K;
+#pragma unroll
+        for (int j = 0; j < K; j++) o[j] = M[j];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// one wave per query: the K best of the nblk blocks' K keys, written as int64 row indices.
+template <int K>
+__global__ void __launch_bounds__(256) rq_merge_kernel(const unsigned long long* __restrict__ cand, int nblk, int M,
+                                                       int64_t* __restrict__ out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= M) return;
+  const int g = q / RQ_QG, ql = q % RQ_QG;
+  unsigned long long L[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) L[j] = ~0ull;
+  for (int b = lane; b < nblk; b += 64) {
+    const unsigned long long* c = cand + ((size_t)(g * nblk + b) * RQ_QG + ql) * K;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const unsigned long long key = c[j];
+      if (key < L[K - 1]) kins<K>(L, key);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) kmerge_xor<K>(L, off);
+  if (lane < K) {
+    unsigned long long v = L[0];
+#pragma unroll
+    for (int j = 1; j < K; j++)
+      if (lane == j) v = L[j];
+    out[(size_t)q * K + lane] = (int64_t)(v & 0xffffffffull);
+  }
+}
+
+}  // namespace m3s
+
+// ------------------------------------------------------------------------------------------
+extern "C" hipError_t m3s_launch_rq_prep(const float* X, int R, int D, int S, int ntiles, int inner_n, uint4* frag,
+                                         hipStream_t s) {
+  const size_t total = (size_t)ntiles * S * 64;
+  hipLaunchKernelGGL(m3s::rq_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, R, D, S, ntiles,
+                     inner_n, frag);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_rq_norm(const float* X, int R, int D, int Rp, float pad_value, float* nrm,
+                                         hipStream_t s) {
+  hipLaunchKernelGGL(m3s::rq_norm_kernel, dim3((Rp + 3) / 4), dim3(256), 0, s, X, R, D, Rp, pad_value, nrm);
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t rq_launch_k(const uint4* cfrag, const float* cn, const uint4* qfrag, const float* qn, int S,
+                              int nblk, int groups, int M, unsigned long long* cand, int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(m3s::rq_gemm_topk_kernel<K>, dim3(nblk, groups), dim3(RQ_THREADS), 0, s, cfrag, cn, qfrag, qn, S,
+                     cand);
+  hipLaunchKernelGGL(m3s::rq_merge_kernel<K>, dim3((M + 3) / 4), dim3(256), 0, s, cand, nblk, M, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_rq_topk(const uint4* cfrag, const float* cn, const uint4* qfrag, const float* qn,
+                                         int S, int nblk, int groups, int M, int k, unsigned long long* cand,
+                                         int64_t* out, hipStream_t s) {
+  switch (k) {
+    case 1: return rq_launch_k<1>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 2: return rq_launch_k<2>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 3: return rq_launch_k<3>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 4: return rq_launch_k<4>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 5: return rq_launch_k<5>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 6: return rq_launch_k<6>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 7: return rq_launch_k<7>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    case 8: return rq_launch_k<8>(cfrag, cn, qfrag, qn, S, nblk, groups, M, cand, out, s);
+    default: return hipErrorInvalidValue;
+  }
+}

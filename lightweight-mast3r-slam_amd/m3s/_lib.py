@@ -81,6 +81,10 @@ _SIGS = {
     "m3s_match_workspace_size": ([c_int] * 4, c_size_t),
     "m3s_match": ([c_void_p] * 7 + [c_int] * 5 + [c_float] * 3 + [c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
     "m3s_track_workspace_size": ([c_int], c_size_t),
+    "m3s_codebook_size": ([c_int, c_int], c_size_t),
+    "m3s_codebook_prepare": ([c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
+    "m3s_quantize_workspace_size": ([c_int] * 4, c_size_t),
+    "m3s_quantize": ([c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "m3s_track": ([ctypes.POINTER(TrackInputs), ctypes.POINTER(TrackConfig), ctypes.POINTER(TrackFuse), c_int,
                    c_void_p, ctypes.POINTER(TrackResult), c_void_p, c_size_t, c_void_p], c_int),
 }

@@ -12,6 +12,7 @@
 """
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -207,3 +208,14 @@ def two_way(G):
     valid = torch.cat((G["valid"], torch.stack(valid_r).to(dev)))
     Q = torch.cat((G["Q"], G["Q"].flip(1)))
     return ii, jj, idx, valid, Q
+
+
+def retrieval_inputs(seed, C, D, M):
+    """Unit-norm fp32 codebook centroids (C, D) and local features (M, D), ASMK-like, from a numpy seed
+    (the retrieval golden fixtures store only the seed, shapes and a checksum)."""
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((C, D)).astype(np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    q = rng.standard_normal((M, D)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    return c, q

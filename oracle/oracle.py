@@ -463,3 +463,24 @@ def backproject_constrain(X, K, img_size):
     t2 = ((v.reshape(-1) - K[1, 2]) / K[1, 1]).astype(np.float32)
     z = X[..., 2]
     return np.stack((z * t1, z * t2, z * 1.0), -1).astype(np.float32)
+
+
+# ---------------------------------------------------------------- retrieval quantization
+def quantize_custom(centroids, qvecs, k, dtype=np.float64):
+    """``RetrievalDatabase.quantize_custom`` (``mast3r_slam/retrieval_database.py:96-105``) in numpy:
+    l2 = (|q|^2 + |c|^2) - 2 q c^T in ``dtype`` (fp64 = the truth the tests measure against), the k
+    smallest per row in ascending order (ties -> lower index). Returns (indices int64 (M, k), l2)."""
+    c = np.asarray(centroids, dtype=dtype)
+    q = np.asarray(qvecs, dtype=dtype)
+    l2 = (np.sum(q * q, axis=1)[:, None] + np.sum(c * c, axis=1)[None, :]) - 2.0 * (q @ c.T)
+    part = np.argpartition(l2, k - 1, axis=1)[:, :k] if k < l2.shape[1] else np.tile(np.arange(l2.shape[1]), (len(l2), 1))
+    rows = np.arange(len(l2))[:, None]
+    order = np.lexsort((part, l2[rows, part]), axis=1)
+    return part[rows, order].astype(np.int64), l2
+
+
+def topk_equivalent(got, ref, l2, tol):
+    """True where ``got`` and ``ref`` pick the same index at each rank, or indices whose fp64 distances
+    differ by at most ``tol`` (a near-tie that any fp32-rounded GEMM may order either way)."""
+    rows = np.arange(len(l2))[:, None]
+    return (got == ref) | (np.abs(l2[rows, got] - l2[rows, ref]) <= tol)

@@ -9,12 +9,15 @@ travels: only the resulting .npz vectors are committed. What runs from the refer
   mast3r_slam/tracker.py      FrameTracker.track / opt_pose_ray_dist_sim3 / opt_pose_calib_sim3 / solve
   mast3r_slam/global_opt.py   FactorGraph.solve_GN_rays / solve_GN_calib (prep_two_way_edges, pin, write-back)
   mast3r_slam/frame.py        Frame.update_pointmap (weighted_pointmap fusion)
+  mast3r_slam/retrieval_database.py  RetrievalDatabase.quantize_custom (distance GEMM + top-k), called
+                              unbound on a stand-in `self` holding the centroids
 
 Stand-ins (the reference's native / third-party pieces cannot run here — no nvcc, no lietorch,
 no ViT checkpoint):
   lietorch               -> oracle/lietorch_shim.py (restated published algorithm; parity unpinned)
   mast3r_slam_backends   -> oracle/m3s_oracle.c via oracle/oracle.py (restated CUDA kernels)
   mast3r_slam.mast3r_utils -> stub; the synthetic "model outputs" are fed to the glue directly.
+  mast3r.retrieval.*, asmk -> stubs (only quantize_custom runs, which needs neither).
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -308,9 +311,37 @@ def gen_ba_rows(N=512, seed=11):
          **{f"{m}_H": v[0] for m, v in out.items()}, **{f"{m}_g": v[1] for m, v in out.items()})
 
 
+# ---------------------------------------------------------------- retrieval quantization
+def gen_retrieval():
+    for name in ("mast3r", "mast3r.retrieval", "mast3r.retrieval.processor", "mast3r.retrieval.model", "asmk",
+                 "asmk.io_helpers"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["mast3r.retrieval.processor"].Retriever = object
+    sys.modules["mast3r.retrieval.model"].how_select_local = None
+    sys.modules["asmk"].io_helpers = sys.modules["asmk.io_helpers"]
+    import mast3r_slam.retrieval_database as ref_rd
+
+    out = {}
+    # (seed, C, D, M, k): ragged codebook / feature sizes, one and two query groups, query and build k
+    cases = [(21, 1000, 200, 37, 5), (22, 2048, 64, 310, 1), (23, 777, 96, 64, 8)]
+    for i, (seed, C, D, M, k) in enumerate(cases):
+        c, q = synthetic.retrieval_inputs(seed, C, D, M)
+        fake = types.SimpleNamespace(centroids=torch.from_numpy(c))
+        idx = ref_rd.RetrievalDatabase.quantize_custom(fake, torch.from_numpy(q), {"quantize": {"multiple_assignment": k}})
+        out[f"case{i}"] = np.array([seed, C, D, M, k])
+        out[f"case{i}_topk"] = _np(idx)
+        out[f"case{i}_checksum"] = np.array([c.astype(np.float64).sum(), q.astype(np.float64).sum()])
+    save("retrieval_quantize.npz", **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["gen_" + name]()
+        sys.exit(0)
     gen_matching()
     gen_tracking()
     gen_opt_pose()
     gen_ba()
     gen_ba_rows()
+    gen_retrieval()
