@@ -29,6 +29,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 matrix-core peak (no sparsity)
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector spec
 
 
@@ -51,6 +52,7 @@ def parse():
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-retrieval", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured HBM-copy / FMA peak probes")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP-event spans inside the timed loop (no roofline)")
@@ -213,6 +215,66 @@ def bench_ba(args, rank, world, dev):
             "scaling": "strong", "mode": "rays"}
 
 
+def bench_retrieval(dev):
+    """RetrievalDatabase.quantize_custom (retrieval_database.py:96-105) at the reference's
+    shapes (64k x 1024 asmk codebook, 300 local features, multiple_assignment 5). Roofline of the fused
+    GEMM + block top-k (+ merge) launch pair: matrix-core flops actually issued (3 bf16 products per fp32
+    product, 304 padded query rows) against the dense bf16 peak, and the codebook stream against HBM."""
+    import torch.nn.functional as F
+
+    from m3s import _lib
+    from m3s.retrieval import Codebook
+
+    C, D, M, k = 65536, 1024, 300, 5
+    g = torch.Generator(device=dev).manual_seed(0)
+    c = F.normalize(torch.randn(C, D, device=dev, generator=g), dim=1)
+    q = F.normalize(torch.randn(M, D, device=dev, generator=g), dim=1)
+    cb = Codebook(c)
+    for _ in range(3):
+        cb.quantize(q, k)
+    torch.cuda.synchronize()
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        cb.quantize(q, k)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    lib = _lib.load()
+    lib.m3s_timing_enable(1)
+    lib.m3s_timing_reset()
+    for _ in range(reps):
+        cb.quantize(q, k)
+    torch.cuda.synchronize()
+    tot, cnt = _lib.c_double(), _lib.c_int()
+    lib.m3s_timing_query(b"quantize_topk", tot, cnt)
+    lib.m3s_timing_enable(0)
+    kms = tot.value / max(cnt.value, 1)
+    mfma_flops = 3 * 2 * ((M + 303) // 304 * 304) * C * D
+    def torch_ref():  # the reference's formulation on the same GPU (fp32 GEMM + topk), for context
+        l2 = torch.sum(q ** 2, dim=1)[:, None] + torch.sum(c ** 2, dim=1)[None, :] - 2 * (q @ c.mT)
+        return torch.topk(l2, k, dim=1, largest=False).indices
+
+    for _ in range(3):
+        torch_ref()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(10):
+        torch_ref()
+    e1.record()
+    e1.synchronize()
+    achieved = mfma_flops / (kms * 1e-3) / 1e12
+    return {"calls_per_s": 1e3 / ms, "ms_per_call": ms, "kernel_ms": kms,
+            "shape": {"codebook": [C, D], "queries": M, "k": k},
+            "dtype": "bf16 hi/lo split (3 MFMA per fp32 product), fp32 accumulate",
+            "roofline": {"kernel": "rq_gemm_topk + rq_merge", "bound": "mfma", "achieved": achieved,
+                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
+                         "alg_TFLOPs": 2.0 * M * C * D / (kms * 1e-3) / 1e12,
+                         "codebook_GBps": C * D * 4 / (kms * 1e-3) / 1e9},
+            "torch_fp32_topk_ms": e0.elapsed_time(e1) / 10}
+
+
 def measured_peaks(dev):
     """re-measure the peaks on the box — a STREAM-like device copy (torch, 2 x 2 GiB) and a
     v_fma_f32 loop (libm3s peak probe, 4 waves per SIMD on every CU)."""
@@ -338,6 +400,7 @@ def main():
     ba = None
     if not args.no_ba:
         ba = bench_ba(args, rank, world, dev)
+    retrieval = bench_retrieval(dev) if (rank == 0 and not args.no_retrieval) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
@@ -355,6 +418,7 @@ def main():
                        "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
             "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,
+            "retrieval": retrieval,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

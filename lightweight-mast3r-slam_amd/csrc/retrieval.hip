@@ -160,8 +160,10 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
         __builtin_amdgcn_global_load_lds((rq_gptr)(ca + (size_t)s * RQ_AU + i * 64), (rq_lptr)&sa_[b][i * 64], 16, 0, 0);
 #endif
       } else {
+#ifndef RQ_EXP_NOBSTAGE  // (experiment builds only) queries staged once: every k-step reuses step 0's image
         __builtin_amdgcn_global_load_lds((rq_gptr)(qa + (size_t)s * RQ_QU + (i - NA) * 64),
                                          (rq_lptr)&sb_[b][(i - NA) * 64], 16, 0, 0);
+#endif
       }
     }
   };
@@ -172,6 +174,12 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
   }
 #endif
   stage(0, 0);
+#ifdef RQ_EXP_NOBSTAGE
+  for (int i = w; i < RQ_QU / 64; i += RQ_THREADS / 64) {
+    __builtin_amdgcn_global_load_lds((rq_gptr)(qa + i * 64), (rq_lptr)&sb_[0][i * 64], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((rq_gptr)(qa + i * 64), (rq_lptr)&sb_[1][i * 64], 16, 0, 0);
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int s = 0; s < S; s++) {

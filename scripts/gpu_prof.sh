@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS=${ARGS:---steps 20 --warmup 5 --no-cpu --no-ba --no-peaks}
+ARGS=${ARGS:---steps 20 --warmup 5 --no-cpu --no-ba --no-peaks --no-retrieval}
 rocprofv3 -L > gpurun_out/prof/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py $ARGS > gpurun_out/prof/trace_bench.json 2> gpurun_out/prof/trace.err
 echo "TRACE_RC=$?"
