@@ -92,6 +92,20 @@ int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, cons
                      const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
                      const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out, void* workspace,
                      size_t workspace_bytes, m3s_ba_plan* plan, void* stream);
+/* Zero-copy keyframe source: instead of the stacked Xs / Cs that
+ * FactorGraph.get_poses_points builds with torch.stack (global_opt.py:114-121), the keyframes' own buffers.
+ * Host arrays of Kp entries: X[k] -> that keyframe's (N,3) X_canon, C[k] -> its (N) confidence sum (device
+ * pointers), N_avg[k] = its fusion count N; the average confidence is C * float32(1/N), exactly
+ * Frame.get_average_conf (frame.py:93-94) on a torch device. Same plan and results as m3s_ba_make_plan. */
+typedef struct m3s_ba_keyframes {
+  const float* const* X;
+  const float* const* C;
+  const float* N_avg;
+} m3s_ba_keyframes;
+int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp, int N,
+                        const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                        const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out, void* workspace,
+                        size_t workspace_bytes, m3s_ba_plan* plan, void* stream);
 int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count);
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);

@@ -462,6 +462,9 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   a->info = c.take<int>(4);
   a->done = a->info + 1;
   a->iters = a->info + 2;
+  a->Xkf = c.take<const float*>(Kp);
+  a->Ckf = c.take<const float*>(Kp);
+  a->Cscale = c.take<float>(Kp);
   return c.off;
 }
 
@@ -474,10 +477,12 @@ extern "C" size_t m3s_ba_workspace_size(int Kp, int N, int E) {
   return ba_carve(c, Kp, N, E, ba_chunks(N, E), &a, &off);
 }
 
-extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
-                                const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
-                                const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
-                                void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+namespace {
+// Keyframe sources (host arrays of Kp entries) -> the plan's device tables.
+int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* Xh, const float* const* Ch,
+                      const float* scale_h, int Kp, int N, const int64_t* ii, const int64_t* jj, int E, int e0, int e1,
+                      const int64_t* idx, const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                      void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
   M3S_CHECK(cfg && plan, "ba: null argument");
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
@@ -550,12 +555,13 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
   HIP_TRY(h2d(P.a.blk_ent, bent.data(), sizeof(int) * bent.size()), "ba upload");
   HIP_TRY(h2d(P.a.rhs_ptr, rptr.data(), sizeof(int) * rptr.size()), "ba upload");
   HIP_TRY(h2d(P.a.rhs_ent, rent.data(), sizeof(int) * rent.size()), "ba upload");
+  HIP_TRY(h2d(P.a.Xkf, Xh, sizeof(const float*) * Kp), "ba upload");
+  HIP_TRY(h2d(P.a.Ckf, Ch, sizeof(const float*) * Kp), "ba upload");
+  HIP_TRY(h2d(P.a.Cscale, scale_h, sizeof(float) * Kp), "ba upload");
   HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
   HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");
   HIP_TRY(hipStreamSynchronize(s), "ba upload sync");  // host vectors die at return
   P.a.Twc = Twc;
-  P.a.Xs = Xs;
-  P.a.Cs = Cs;
   P.a.idx = idx;
   P.a.valid = valid;
   P.a.Q = Q;
@@ -591,6 +597,37 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
   HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
   memcpy(plan->opaque, &P, sizeof(P));
   return M3S_OK;
+}
+}  // namespace
+
+extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                                const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                                const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                                void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(Xs && Cs && Kp >= 1 && N >= 1, "ba: null Xs/Cs or bad sizes");
+  std::vector<const float*> xh(Kp), ch(Kp);
+  std::vector<float> sh(Kp, 1.0f);  // stacked Cs is already the average confidence
+  for (int k = 0; k < Kp; k++) {
+    xh[k] = Xs + (size_t)k * N * 3;
+    ch[k] = Cs + (size_t)k * N;
+  }
+  return ba_make_plan_impl(cfg, Twc, xh.data(), ch.data(), sh.data(), Kp, N, ii, jj, E, e0, e1, idx, valid, Q,
+                           delta_thresh, dx_out, workspace, workspace_bytes, plan, stream);
+}
+
+extern "C" int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp, int N,
+                                   const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                                   const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                                   void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(kf && kf->X && kf->C && kf->N_avg && Kp >= 1 && N >= 1, "ba: null keyframe table or bad sizes");
+  std::vector<float> sh(Kp);
+  for (int k = 0; k < Kp; k++) {
+    M3S_CHECK(kf->X[k] && kf->C[k], "ba: null keyframe buffer");
+    M3S_CHECK(kf->N_avg[k] > 0.0f, "ba: keyframe fusion count N must be positive");
+    sh[k] = 1.0f / kf->N_avg[k];  // torch's C / N on a device tensor: C * float32(1/N)
+  }
+  return ba_make_plan_impl(cfg, Twc, kf->X, kf->C, sh.data(), Kp, N, ii, jj, E, e0, e1, idx, valid, Q, delta_thresh,
+                           dx_out, workspace, workspace_bytes, plan, stream);
 }
 
 extern "C" int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count) {

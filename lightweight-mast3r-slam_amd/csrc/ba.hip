@@ -73,10 +73,10 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
     const int ix = a.ii_rank[e], jx = a.jj_rank[e];
     const bool vm = a.valid[g] != 0;
     const int64_t ind = vm ? a.idx[g] : 0;
-    const float* Xi = a.Xs + ((size_t)ix * N + ind) * 3;
+    const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
     const float q = a.Q[g];
-    const bool valid = vm && (q > p.Q_thresh) && (a.Cs[(size_t)ix * N + ind] > p.C_thresh) &&
-                       (a.Cs[(size_t)jx * N + k] > p.C_thresh);
+    const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
+                       (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
     // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
     const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
     float4 r;
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
   const float4* rec = a.rec + (size_t)e * N;
-  const float* Xj_base = a.Xs + (size_t)jx * N * 3;
+  const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
   const int k_end = min(N, k_begin + per);

@@ -21,8 +21,9 @@ struct BaParams {
 
 struct BaArgs {
   float* Twc;            // (K,8) in/out
-  const float* Xs;       // (K,N,3)
-  const float* Cs;       // (K,N)
+  const float* const* Xkf;  // (K) -> (N,3) keyframe points: rows of the stacked Xs, or each keyframe's X_canon
+  const float* const* Ckf;  // (K) -> (N)   confidences: rows of the stacked Cs, or each keyframe's C sum
+  const float* Cscale;      // (K) 1 (stacked Cs) or float32(1/N_k) (get_average_conf on a torch device: C * (1/N))
   const int* ii_rank;    // (E_local) dense rank of i (pin 0), shard-local
   const int* jj_rank;    // (E_local)
   const int64_t* idx;    // (E,N) global edge rows

@@ -25,6 +25,10 @@ class BaConfig(ctypes.Structure):
                 ("height", c_int), ("width", c_int), ("pixel_border", c_int), ("z_eps", c_float)]
 
 
+class BaKeyframes(ctypes.Structure):
+    _fields_ = [("X", ctypes.POINTER(c_void_p)), ("C", ctypes.POINTER(c_void_p)), ("N_avg", ctypes.POINTER(c_float))]
+
+
 class BaPlan(ctypes.Structure):
     _fields_ = [("opaque", ctypes.c_ubyte * 768)]
 
@@ -73,6 +77,9 @@ _SIGS = {
     "m3s_ba_make_plan": ([ctypes.POINTER(BaConfig), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                           c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                           c_void_p, c_size_t, ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_make_plan_kf": ([ctypes.POINTER(BaConfig), c_void_p, ctypes.POINTER(BaKeyframes), c_int, c_int, c_void_p,
+                             c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                             c_void_p, c_size_t, ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_edge_sums": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)], c_int),
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),

@@ -15,6 +15,7 @@ The backend is pluggable so the protocol itself can be exercised on CPU with ``g
 an oracle backend); the product backend is ``HipShard`` over ``libm3s.so``.
 """
 import ctypes
+from ctypes import c_void_p
 
 import torch
 import torch.distributed as dist
@@ -48,26 +49,45 @@ def ba_config(mode, cfg, K=None, height=0, width=0):
 
 
 class HipShard:
-    """One rank's view of a sharded BA problem on its GPU (libm3s split API)."""
+    """One rank's view of a sharded BA problem on its GPU (libm3s split API).
 
-    def __init__(self, cfg_struct, Twc, Xs, Cs, ii, jj, idx, valid, Q, delta_thresh, e0, e1):
+    The keyframe points come either stacked (``Xs`` (K,N,3), ``Cs`` (K,N) average confidences, as
+    ``get_poses_points`` builds them) or, with ``Xs=None``, zero-copy from the keyframes' own buffers:
+    ``keyframes = (X_list, C_list, N_list)`` with each X (N,3), C (N or N,1) the confidence sum and N the
+    fusion count (``m3s_ba_make_plan_kf``)."""
+
+    def __init__(self, cfg_struct, Twc, Xs, Cs, ii, jj, idx, valid, Q, delta_thresh, e0, e1, keyframes=None):
         lib = _lib.load()
         self.lib = lib
         self.dev = Twc.device
-        Kp, N = Xs.shape[0], Xs.shape[1]
+        if Xs is None:
+            X_list, C_list, N_list = keyframes
+            Kp, N = len(X_list), X_list[0].shape[-2]
+            for x, cc in zip(X_list, C_list):
+                if x.dtype != torch.float32 or cc.dtype != torch.float32 or not x.is_contiguous() or \
+                        not cc.is_contiguous() or x.numel() != 3 * N or cc.numel() != N:
+                    raise RuntimeError("ba: keyframe X (N,3) / C (N) must be contiguous float32")
+        else:
+            Kp, N = Xs.shape[0], Xs.shape[1]
         E = ii.shape[0]
         self.Kp, self.E = Kp, E
         self.dx = torch.zeros((max(Kp - 1, 0), 7), dtype=torch.float32, device=self.dev)
         nbytes = lib.m3s_ba_workspace_size(Kp, N, E)
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
-        self.keep = (Twc, Xs, Cs, ii, jj, idx, valid, Q)
+        self.keep = (Twc, Xs, Cs, ii, jj, idx, valid, Q, keyframes)
         self.plan = _lib.BaPlan()
         self.cfg = cfg_struct
-        _lib.check(lib.m3s_ba_make_plan(ctypes.byref(cfg_struct), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs), Kp, N,
-                                        _lib.ptr(ii), _lib.ptr(jj), E, int(e0), int(e1), _lib.ptr(idx),
-                                        _lib.ptr(valid), _lib.ptr(Q), float(delta_thresh), _lib.ptr(self.dx),
-                                        _lib.ptr(self.ws), self.ws.numel(), ctypes.byref(self.plan),
-                                        _lib.stream_ptr(self.dev)))
+        tail = (_lib.ptr(ii), _lib.ptr(jj), E, int(e0), int(e1), _lib.ptr(idx), _lib.ptr(valid), _lib.ptr(Q),
+                float(delta_thresh), _lib.ptr(self.dx), _lib.ptr(self.ws), self.ws.numel(), ctypes.byref(self.plan),
+                _lib.stream_ptr(self.dev))
+        if Xs is None:
+            kt = _lib.BaKeyframes((c_void_p * Kp)(*[x.data_ptr() for x in X_list]),
+                                  (c_void_p * Kp)(*[cc.data_ptr() for cc in C_list]),
+                                  (ctypes.c_float * Kp)(*[float(n) for n in N_list]))
+            _lib.check(lib.m3s_ba_make_plan_kf(ctypes.byref(cfg_struct), _lib.ptr(Twc), ctypes.byref(kt), Kp, N, *tail))
+        else:
+            _lib.check(lib.m3s_ba_make_plan(ctypes.byref(cfg_struct), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs), Kp, N,
+                                            *tail))
         off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
         _lib.check(lib.m3s_ba_edge_sums(ctypes.byref(self.plan), ctypes.byref(off), ctypes.byref(cnt)))
         self.edge_sums = self.ws[off.value: off.value + cnt.value].view(torch.float64)
@@ -96,14 +116,17 @@ def run_sharded(shard, max_iter, group=None):
 
 
 def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter, delta_thresh, K=None, height=0,
-                         width=0, group=None):
+                         width=0, group=None, keyframes=None):
     """Multi-GPU drop-in for mast3r_slam_backends.gauss_newton_*: same inputs (every rank holds the
-    full problem, replicated), Twc updated in place identically on every rank; returns [dx]."""
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    full problem, replicated), Twc updated in place identically on every rank; returns [dx]. With
+    ``Xs=None`` the keyframe points come zero-copy from ``keyframes`` (see ``HipShard``)."""
+    rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     e0, e1 = shard_range(ii.shape[0], rank, world)
     c = lambda t: t.contiguous()
-    shard = HipShard(ba_config(mode, cfg, K, height, width), c(Twc), c(Xs), c(Cs.reshape(Xs.shape[0], -1)), c(ii),
-                     c(jj), c(idx), c(valid.reshape(idx.shape)), c(Q.reshape(idx.shape)), delta_thresh, e0, e1)
+    if Xs is not None:
+        Xs, Cs = c(Xs), c(Cs.reshape(Xs.shape[0], -1))
+    shard = HipShard(ba_config(mode, cfg, K, height, width), c(Twc), Xs, Cs, c(ii), c(jj), c(idx),
+                     c(valid.reshape(idx.shape)), c(Q.reshape(idx.shape)), delta_thresh, e0, e1, keyframes=keyframes)
     run_sharded(shard, max_iter, group)
     return [shard.dx]

@@ -102,18 +102,43 @@ class FactorGraph:
         Cs = torch.stack([kf.get_average_conf() for kf in kfs])
         return Xs, T_WCs, Cs
 
+    def get_poses_keyframes(self, unique_kf_idx):
+        """Zero-copy counterpart of get_poses_points: the poses are stacked (K x 8
+        floats) but the points stay in the keyframes' own X_canon / C buffers, which the BA plan reads
+        through a pointer table (``m3s_ba_make_plan_kf``); the average confidence C / N is applied in the
+        pack kernel. Returns None when a keyframe's buffers do not qualify (then the stacked path runs)."""
+        kfs = [self.frames[int(i)] for i in unique_kf_idx]
+        X = [kf.X_canon for kf in kfs]
+        C = [kf.C for kf in kfs]
+        ok = all(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and c.dtype == torch.float32 and
+                 c.is_contiguous() and x.numel() == X[0].numel() and c.numel() * 3 == x.numel() for x, c in zip(X, C))
+        if not ok:
+            return None
+        T_WCs = Sim3(torch.stack([kf.T_WC.data.reshape(1, 8) for kf in kfs]))
+        return T_WCs, (X, C, [float(kf.N) for kf in kfs])
+
     def _sharded(self):
         return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
 
     def solve_GN_rays(self):
-        """global_opt.py:123-161."""
+        """global_opt.py:123-161, with the keyframe points read in place (no torch.stack of K x N x 16 B)."""
         cfg = self.cfg
         pin = cfg["pin"]
         unique_kf_idx = self.get_unique_kf_idx()
         if unique_kf_idx.numel() <= pin:
             return
-        Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
         ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
+        zc = self.get_poses_keyframes(unique_kf_idx)
+        if zc is not None:
+            from m3s.dist_ba import gauss_newton_sharded
+
+            T_WCs, keyframes = zc
+            gauss_newton_sharded("rays", T_WCs.data[:, 0, :], None, None, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
+                                 cfg, cfg["max_iters"], cfg["delta_norm"],
+                                 group=self.group, keyframes=keyframes)
+            self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])
+            return
+        Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
         pose_data = T_WCs.data[:, 0, :]
         if self._sharded():
             from m3s.dist_ba import gauss_newton_sharded

@@ -253,3 +253,28 @@ def test_ba_medium_graph_vs_fp64_truth(mode):
     T, dx = _call(mode, G["Twc0"].numpy(), Xs, Cs, ii, jj, idx, valid, Q, K, H, W)
     assert np.isfinite(T).all()
     np.testing.assert_allclose(T, T_ref, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_zero_copy_keyframe_plan_equals_stacked(golden):
+    """m3s_ba_make_plan_kf (keyframes' own X_canon / C-sum buffers) == the stacked plan
+    of get_poses_points, bit for bit, including the average confidence C / N with N > 1."""
+    from m3s.config import config
+    from m3s.dist_ba import gauss_newton_sharded
+
+    g = golden("ba_6kf_24x32.npz")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    K = g["Xs"].shape[0]
+    Nfuse = [1, 3, 2, 7, 1, 5]
+    X_list = [d(g["Xs"][k]) for k in range(K)]
+    C_sum = [d(g["Cs"][k]) * float(n) for k, n in enumerate(Nfuse)]        # keyframe confidence sums
+    Cs = torch.stack([c / n for c, n in zip(C_sum, Nfuse)])                # get_average_conf, stacked
+    Xs = torch.stack(X_list)
+    ii2, jj2 = d(np.concatenate((g["ii"], g["jj"]))), d(np.concatenate((g["jj"], g["ii"])))
+    args = (ii2, jj2, d(g["idx2"]), d(g["valid2"]), d(g["Q2"]), config["local_opt"], 10, 1e-8)
+    T_a, T_b = d(g["Twc0"]), d(g["Twc0"])
+    dx_a = gauss_newton_sharded("rays", T_a, Xs, Cs, *args)[0]
+    dx_b = gauss_newton_sharded("rays", T_b, None, None, *args, keyframes=(X_list, C_sum, Nfuse))[0]
+    assert torch.equal(T_a, T_b) and torch.equal(dx_a, dx_b)
+    with pytest.raises(RuntimeError):
+        gauss_newton_sharded("rays", d(g["Twc0"]), None, None, *args, keyframes=(X_list, C_sum, [1, 0, 1, 1, 1, 1]))
