@@ -166,7 +166,7 @@ KERNEL_SYMBOL = {"prep_rays": "prep_rays_kernel", "proj_occlusion": "proj_occlus
 def pmc_traffic(name):
     """HBM bytes per launch of `name` from the newest committed rocprofv3 PMC summary
     (profiles/<round>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, scripts/profile_summary.py); None if absent."""
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc.json")))
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r[0-9][0-9]_pmc.json")))
     if not files:
         return None
     for k, v in json.load(open(files[-1])).items():
