@@ -20,8 +20,9 @@
 //   * One 512-thread block per 256 codebook rows (256 blocks = one per CU at 64k rows), two waves
 //     per SIMD: wave w owns 32 rows (two 16-row tiles) against all 19 query tiles of the group, i.e.
 //     38 16x16 fp32 accumulator tiles = 152 registers per lane (no spills at 256 per wave).
-//     Codebook (32 KB) and query (38 KB) k-step images are double-buffered in LDS; each query
-//     fragment pair read feeds 6 MFMAs, each codebook fragment pair 57.
+//     Query k-step images (38 KB) are double-buffered in LDS (global_load_lds one step ahead); each wave's
+//     codebook fragments (4 KB per step) stream global -> VGPR two steps ahead through a 3-slot register ring.
+//     Each query fragment pair read feeds 6 MFMAs, each codebook fragment pair 57.
 //   * Epilogue (exact block top-k per query, keys = order-preserving fp32 bits << 32 | row): a
 //     query's 256 block distances sit in 32 lanes, 8 each. tau = the k-th smallest of the 32 lane
 //     minima bounds the k-th best, so only distances <= tau (typically ~6 per query and block) are
@@ -31,10 +32,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace m3s {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const void* rq_gptr;
 typedef __attribute__((address_space(3))) void* rq_lptr;
 
@@ -140,58 +144,47 @@ template <int K>
 __global__ void __launch_bounds__(RQ_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ cn, const uint4* __restrict__ qfrag,
                     const float* __restrict__ qn, int S, unsigned long long* __restrict__ cand) {
-  __shared__ uint4 sb_[2][RQ_QU];  // query k-step images
-  __shared__ uint4 sa_[2][RQ_AU];  // codebook k-step images
+  // query k-step images: two separate arrays (not one indexed by parity) so the compiler can prove that a
+  // step's ds_reads never alias the global_load_lds writing the other image; with one array it waits
+  // vmcnt(0) before every read and the staging no longer overlaps the MFMAs
+  __shared__ uint4 sb0_[RQ_QU];
+  __shared__ uint4 sb1_[RQ_QU];
+  __shared__ uint4 sa_[2][RQ_AU];  // epilogue scratch (candidate lists)
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int g = blockIdx.y;
-  const uint4* ca = cfrag + (size_t)blockIdx.x * S * RQ_AU + lane;
+  // this wave's codebook units of a k-step: tiles 2w, 2w+1 x {hi, lo} = 4 x 1 KB, contiguous
+  const uint4* ca = cfrag + (size_t)blockIdx.x * S * RQ_AU + (size_t)(w * RQ_NR * 2) * 64 + lane;
   const uint4* qa = qfrag + (size_t)g * S * RQ_QU + lane;
-  constexpr int NA = RQ_AU / 64, NCP = NA + RQ_QU / 64;  // 1-KB wave copies per k-step: 32 codebook + 38 query
   f4v acc[RQ_NR][RQ_NQT];
 #pragma unroll
   for (int r = 0; r < RQ_NR; r++)
 #pragma unroll
     for (int q = 0; q < RQ_NQT; q++) acc[r][q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-  // k-step images: lane-linear 1-KB global_load_lds copies dealt round-robin to the 8 waves
-  auto stage = [&](int s, int b) {
-    for (int i = w; i < NCP; i += RQ_THREADS / 64) {
-      if (i < NA) {
-#ifndef RQ_EXP_NOLOAD  // (experiment builds only) no codebook stream: every k-step reuses step 0's image
-        __builtin_amdgcn_global_load_lds((rq_gptr)(ca + (size_t)s * RQ_AU + i * 64), (rq_lptr)&sa_[b][i * 64], 16, 0, 0);
-#endif
-      } else {
-#ifndef RQ_EXP_NOBSTAGE  // (experiment builds only) queries staged once: every k-step reuses step 0's image
-        __builtin_amdgcn_global_load_lds((rq_gptr)(qa + (size_t)s * RQ_QU + (i - NA) * 64),
-                                         (rq_lptr)&sb_[b][(i - NA) * 64], 16, 0, 0);
-#endif
-      }
+  // queries: lane-linear 1-KB global_load_lds copies into the idle LDS image, one k-step ahead
+  // (issued by inline asm: the compiler's own wait insertion would otherwise drain every outstanding load with
+  // vmcnt(0) before any read of either image, serialising the staging; the explicit waits below order them)
+  auto stage_b = [&](int s, uint4* dst) {
+    for (int i = w; i < RQ_QU / 64; i += RQ_THREADS / 64) {
+      const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(rq_lptr)&dst[i * 64]);
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(qa + (size_t)s * RQ_QU + i * 64)
+                   : "memory", "m0");
     }
   };
-#ifdef RQ_EXP_NOLOAD
-  for (int i = w; i < NA; i += RQ_THREADS / 64) {
-    __builtin_amdgcn_global_load_lds((rq_gptr)(ca + i * 64), (rq_lptr)&sa_[0][i * 64], 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((rq_gptr)(ca + i * 64), (rq_lptr)&sa_[1][i * 64], 16, 0, 0);
-  }
-#endif
-  stage(0, 0);
-#ifdef RQ_EXP_NOBSTAGE
-  for (int i = w; i < RQ_QU / 64; i += RQ_THREADS / 64) {
-    __builtin_amdgcn_global_load_lds((rq_gptr)(qa + i * 64), (rq_lptr)&sb_[0][i * 64], 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((rq_gptr)(qa + i * 64), (rq_lptr)&sb_[1][i * 64], 16, 0, 0);
-  }
-#endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int s = 0; s < S; s++) {
-    const int buf = s & 1;
-    if (s + 1 < S) stage(s + 1, buf ^ 1);  // in flight behind this step's MFMAs
-    bf16x8 ah[RQ_NR], al[RQ_NR];
+  // codebook: global -> VGPR two k-steps ahead (a 3-slot register ring), by inline-asm loads the compiler does
+  // not wait for: every step ends with s_waitcnt vmcnt(4), which leaves exactly the 4 loads of step s+2 in
+  // flight and retires everything older (the query copies of step s+1 and the codebook of step s+1).
+  auto aload = [&](u32x4 (&A)[4], int s) {
+    const uint4* src = ca + (size_t)s * RQ_AU;
 #pragma unroll
-    for (int r = 0; r < RQ_NR; r++) {
-      ah[r] = __builtin_bit_cast(bf16x8, sa_[buf][((w * RQ_NR + r) * 2) * 64 + lane]);
-      al[r] = __builtin_bit_cast(bf16x8, sa_[buf][((w * RQ_NR + r) * 2 + 1) * 64 + lane]);
-    }
-    const uint4* sb = &sb_[buf][lane];
+    for (int j = 0; j < 4; j++) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(A[j]) : "v"(src + j * 64) : "memory");
+  };
+  auto step = [&](auto parity, int s, const u32x4 (&Ac)[4], u32x4 (&An)[4]) {
+    constexpr int buf = decltype(parity)::value;  // == s & 1
+    if (s + 1 < S) stage_b(s + 1, buf ? sb0_ : sb1_);
+    aload(An, min(s + 2, S - 1));  // past the end: a harmless re-load keeps the vmcnt arithmetic fixed
+    const bf16x8 ah[RQ_NR] = {__builtin_bit_cast(bf16x8, Ac[0]), __builtin_bit_cast(bf16x8, Ac[2])};
+    const bf16x8 al[RQ_NR] = {__builtin_bit_cast(bf16x8, Ac[1]), __builtin_bit_cast(bf16x8, Ac[3])};
+    const uint4* sb = (buf ? sb1_ : sb0_) + lane;
     uint4 bh = sb[0], bl = sb[64];
 #pragma unroll
     for (int q = 0; q < RQ_NQT; q++) {
@@ -210,9 +203,28 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
       bh = nh;
       bl = nl;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k-step s+1 staged (this wave's copies) ...
-    __syncthreads();                                  // ... and every wave's; buffer `buf` no longer read
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");  // this wave's k-step s+1 query copies landed ...
+    __builtin_amdgcn_s_barrier();                      // ... and every wave's; image `buf` no longer read
+    asm volatile("" ::: "memory");
+  };
+  const std::integral_constant<int, 0> I0;
+  const std::integral_constant<int, 1> I1;
+  u32x4 A0[4], A1[4], A2[4];
+  aload(A0, 0);
+  aload(A1, min(1, S - 1));
+  stage_b(0, sb0_);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < S; s += 6) {  // 6 = lcm(3 register slots, 2 LDS images): every selection compile-time
+    step(I0, s, A0, A2);
+    if (s + 1 < S) step(I1, s + 1, A1, A0);
+    if (s + 2 < S) step(I0, s + 2, A2, A1);
+    if (s + 3 < S) step(I1, s + 3, A0, A2);
+    if (s + 4 < S) step(I0, s + 4, A1, A0);
+    if (s + 5 < S) step(I1, s + 5, A2, A1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-loads
+  __syncthreads();
 
   // ---- epilogue: exact block top-K per query by a threshold filter ----
 #ifdef RQ_EXP_NOEPI  // (experiment builds only) skip the top-k: one checksum store per lane
@@ -239,12 +251,13 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
   for (int r = 0; r < RQ_NR; r++)
 #pragma unroll
     for (int i = 0; i < 4; i++) cv[r][i] = cn[row0 + 16 * r + i];
-  float* smin = reinterpret_cast<float*>(&sb_[0][0]);  // [RQ_QG][RQ_NL] lane minima
-  float* tau = smin + RQ_QG * RQ_NL;                   // [RQ_QG]
-  int* cnt = reinterpret_cast<int*>(tau + RQ_QG);      // [RQ_QG] list lengths
-  int* ovf = cnt + RQ_QG;                              // [32] query-tile overflow flags
+  float* smin = reinterpret_cast<float*>(&sb0_[0]);  // [RQ_QG][RQ_NL] lane minima
+  float* tau = reinterpret_cast<float*>(&sb1_[0]);   // [RQ_QG]
+  int* cnt = reinterpret_cast<int*>(tau + RQ_QG);    // [RQ_QG] list lengths
+  int* ovf = cnt + RQ_QG;                            // [32] query-tile overflow flags
   unsigned long long* lst = reinterpret_cast<unsigned long long*>(&sa_[0][0]);  // [RQ_QG][RQ_CAP]
-  static_assert(4 * (RQ_QG * (RQ_NL + 2) + 32) <= (int)sizeof(sb_), "epilogue scalars fit the query images");
+  static_assert(4 * RQ_QG * RQ_NL <= (int)sizeof(sb0_), "lane minima fit a query image");
+  static_assert(4 * (2 * RQ_QG + 32) <= (int)sizeof(sb1_), "epilogue scalars fit a query image");
   static_assert(8 * RQ_QG * RQ_CAP <= (int)sizeof(sa_), "candidate lists fit the codebook images");
   static_assert(8 * 16 * K <= RQ_QG * RQ_CAP, "fallback lists fit the candidate lists");
   const int col = lane & 15, lg = w * 4 + (lane >> 4);  // query column in the tile; lane slot of the query
