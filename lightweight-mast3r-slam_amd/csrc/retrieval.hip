@@ -167,7 +167,7 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
     for (int i = w; i < RQ_QU / 64; i += RQ_THREADS / 64) {
       const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(rq_lptr)&dst[i * 64]);
       asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(qa + (size_t)s * RQ_QU + i * 64)
-                   : "memory", "m0");
+                   : "memory");  // m0 is reserved (never allocated) by the compiler: no clobber needed
     }
   };
   // codebook: global -> VGPR two k-steps ahead (a 3-slot register ring), by inline-asm loads the compiler does
