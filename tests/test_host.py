@@ -33,7 +33,9 @@ def test_workspace_sizes_are_monotone():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name, args in (("m3s_match_workspace_size", [(1, 64, 64, 24), (2, 64, 64, 24), (1, 512, 512, 24)]),
                        ("m3s_track_workspace_size", [(1024,), (4096,), (262144,)]),
-                       ("m3s_ba_workspace_size", [(4, 1024, 6), (8, 1024, 20), (256, 196608, 2000)])):
+                       ("m3s_ba_workspace_size", [(4, 1024, 6), (8, 1024, 20), (256, 196608, 2000)]),
+                       ("m3s_codebook_size", [(100, 64), (1000, 200), (65536, 1024)]),
+                       ("m3s_quantize_workspace_size", [(100, 64, 10, 1), (1000, 64, 310, 5), (65536, 1024, 300, 8)])):
         fn = getattr(lib, name)
         fn.restype = ctypes.c_size_t
         sizes = [fn(*a) for a in args]
@@ -185,3 +187,28 @@ def test_se3_is_sim3_with_unit_scale_and_as_se3_pattern():
                                atol=1e-12, rtol=0)
     torch.testing.assert_close(E.matrix(), T.matrix())
     assert lietorch.Sim3.embedded_dim == 8 and lietorch.SE3.embedded_dim == 7
+
+
+def test_retrieval_abi_validates_before_any_launch():
+    """m3s_codebook_* / m3s_quantize reject bad sizes, k and buffers with an error code and a message before
+    touching the device (runs without a GPU)."""
+    from m3s import _lib
+
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.m3s_last_error.restype = ctypes.c_char_p
+    for name in ("m3s_codebook_size", "m3s_quantize_workspace_size"):
+        getattr(lib, name).restype = ctypes.c_size_t
+    assert lib.m3s_codebook_size(0, 64) == 0 and lib.m3s_quantize_workspace_size(10, 64, 5, 0) == 0
+    buf = ctypes.create_string_buffer(16)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    q = ctypes.c_void_p
+    rc = lib.m3s_quantize(p, 10, 64, p, 5, 9, p, p, ctypes.c_size_t(1 << 30), q(0))
+    assert rc != 0 and b"multiple_assignment" in lib.m3s_last_error()
+    rc = lib.m3s_quantize(p, 4, 64, p, 5, 5, p, p, ctypes.c_size_t(1 << 30), q(0))
+    assert rc != 0 and b"larger than the codebook" in lib.m3s_last_error()
+    rc = lib.m3s_quantize(p, 100, 64, p, 5, 5, p, p, ctypes.c_size_t(16), q(0))
+    assert rc != 0 and b"workspace too small" in lib.m3s_last_error()
+    rc = lib.m3s_codebook_prepare(p, 100, 64, p, ctypes.c_size_t(16), q(0))
+    assert rc != 0 and b"too small" in lib.m3s_last_error()
+    rc = lib.m3s_quantize(q(0), 100, 64, p, 5, 5, p, p, ctypes.c_size_t(1 << 30), q(0))
+    assert rc != 0 and b"null" in lib.m3s_last_error()
