@@ -370,33 +370,61 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
   }
 }
 
-// one wave per query: the K best of the nblk blocks' K keys, written as int64 row indices.
+// one wave per query: the K best of the nblk blocks' K keys (each block list sorted ascending), written as int64
+// row indices. Lane l holds the lists of blocks l + 64 m; K rounds of: wave minimum of the lanes' head keys
+// (keys are unique: they carry the row), the owning lane pops its head.
+#define RQ_ML 4  // block lists per lane (nblk <= 64 * RQ_ML per pass; more blocks are folded in first)
 template <int K>
 __global__ void __launch_bounds__(256) rq_merge_kernel(const unsigned long long* __restrict__ cand, int nblk, int M,
                                                        int64_t* __restrict__ out) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (q >= M) return;
   const int g = q / RQ_QG, ql = q % RQ_QG;
-  unsigned long long L[K];
+  unsigned long long L[RQ_ML][K];
 #pragma unroll
-  for (int j = 0; j < K; j++) L[j] = ~0ull;
-  for (int b = lane; b < nblk; b += 64) {
+  for (int m = 0; m < RQ_ML; m++) {
+    const int b = lane + 64 * m;
+    const unsigned long long* c = cand + ((size_t)(g * nblk + min(b, nblk - 1)) * RQ_QG + ql) * K;
+#pragma unroll
+    for (int j = 0; j < K; j++) L[m][j] = b < nblk ? c[j] : ~0ull;
+  }
+  for (int b = lane + 64 * RQ_ML; b < nblk; b += 64) {  // codebooks beyond 64k rows: fold into list 0
     const unsigned long long* c = cand + ((size_t)(g * nblk + b) * RQ_QG + ql) * K;
 #pragma unroll
     for (int j = 0; j < K; j++) {
       const unsigned long long key = c[j];
-      if (key < L[K - 1]) kins<K>(L, key);
+      if (key < L[0][K - 1]) kins<K>(L[0], key);
     }
   }
+  unsigned long long res = ~0ull;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) kmerge_xor<K>(L, off);
-  if (lane < K) {
-    unsigned long long v = L[0];
+  for (int r = 0; r < K; r++) {
+    unsigned long long h = L[0][0];
+    int hm = 0;
 #pragma unroll
-    for (int j = 1; j < K; j++)
-      if (lane == j) v = L[j];
-    out[(size_t)q * K + lane] = (int64_t)(v & 0xffffffffull);
+    for (int m = 1; m < RQ_ML; m++)
+      if (L[m][0] < h) {
+        h = L[m][0];
+        hm = m;
+      }
+    unsigned long long wmin = h;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long o = __shfl_xor(wmin, off, 64);
+      wmin = o < wmin ? o : wmin;
+    }
+    if (lane == r) res = wmin;
+    if (h == wmin) {  // this lane owns the minimum: pop that list's head
+#pragma unroll
+      for (int m = 0; m < RQ_ML; m++)
+        if (m == hm) {
+#pragma unroll
+          for (int j = 0; j + 1 < K; j++) L[m][j] = L[m][j + 1];
+          L[m][K - 1] = ~0ull;
+        }
+    }
   }
+  if (lane < K) out[(size_t)q * K + lane] = (int64_t)(res & 0xffffffffull);
 }
 
 }  // namespace m3s
