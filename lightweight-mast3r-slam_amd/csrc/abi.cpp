@@ -34,8 +34,7 @@ hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
-hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, hipStream_t);
-hipError_t m3s_launch_rq_norm(const float*, int, int, int, float, float*, hipStream_t);
+hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, int, float, float*, hipStream_t);
 hipError_t m3s_launch_rq_topk(const uint4*, const float*, const uint4*, const float*, int, int, int, int, int,
                               unsigned long long*, int64_t*, hipStream_t);
 }
@@ -741,8 +740,8 @@ extern "C" int m3s_codebook_prepare(const float* centroids, int C, int D, void* 
   codebook_carve(c, C, D, &frag, &cn);
   hipStream_t s = (hipStream_t)stream;
   const int Cp = rq_rows_padded(C);
-  HIP_TRY(m3s_launch_rq_prep(centroids, C, D, rq_steps(D), Cp / 16, RQ_ROWS / 16, frag, s), "codebook prep launch");
-  HIP_TRY(m3s_launch_rq_norm(centroids, C, D, Cp, __builtin_inff(), cn, s), "codebook norm launch");
+  HIP_TRY(m3s_launch_rq_prep(centroids, C, D, rq_steps(D), Cp / 16, RQ_ROWS / 16, frag, Cp, __builtin_inff(), cn, s),
+          "codebook prep launch");
   return M3S_OK;
 }
 
@@ -774,8 +773,8 @@ extern "C" int m3s_quantize(const void* codebook, int C, int D, const float* qve
   quantize_carve(c, C, D, M, k, &qfrag, &qn, &cand);
   hipStream_t s = (hipStream_t)stream;
   const int G = rq_groups(M), S = rq_steps(D);
-  HIP_TRY(m3s_launch_rq_prep(qvecs, M, D, S, G * RQ_NQT, RQ_NQT, qfrag, s), "quantize prep launch");
-  HIP_TRY(m3s_launch_rq_norm(qvecs, M, D, G * RQ_QG, 0.0f, qn, s), "quantize norm launch");
+  HIP_TRY(m3s_launch_rq_prep(qvecs, M, D, S, G * RQ_NQT, RQ_NQT, qfrag, G * RQ_QG, 0.0f, qn, s),
+          "quantize prep launch");
   {
     Span sp("quantize_topk", s);
     HIP_TRY(m3s_launch_rq_topk(cfrag, cn, qfrag, qn, S, rq_rows_padded(C) / RQ_ROWS, G, M, k, cand, topk_out, s),

@@ -76,7 +76,32 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4& hi, uint4& lo
 // * 64 + l: inner_n = RQ_BT for the codebook (a block's k-step contiguous, 32 KB), RQ_NQT for the
 // queries (a group's k-step contiguous, 38 KB). Rows >= R and columns >= D are zero.
 __global__ void __launch_bounds__(256) rq_prep_kernel(const float* __restrict__ X, int R, int D, int S, int ntiles,
-                                                      int inner_n, uint4* __restrict__ frag) {
+                                                      int inner_n, uint4* __restrict__ frag, int nfrag, int Rp,
+                                                      float pad_value, float* __restrict__ nrm) {
+  // blocks [nfrag, ..): the squared row norms |x_r|^2 in fp32, one wave per row; rows in [R, Rp) get pad_value
+  // (+inf for the codebook, so padded rows never rank; 0 for padded queries, whose results are not written)
+  if ((int)blockIdx.x >= nfrag) {
+    const int row = (blockIdx.x - nfrag) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= Rp) return;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    if (row < R) {
+      const float* x = X + (size_t)row * D;
+      int k = lane;
+      for (; k + 192 < D; k += 256) {
+        const float a = x[k], b = x[k + 64], c = x[k + 128], d = x[k + 192];
+        s0 += a * a;
+        s1 += b * b;
+        s2 += c * c;
+        s3 += d * d;
+      }
+      for (; k < D; k += 64) s0 += x[k] * x[k];
+    }
+    float s = (s0 + s1) + (s2 + s3);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) nrm[row] = row < R ? s : pad_value;
+    return;
+  }
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t total = (size_t)ntiles * S * 64;
   if (gid >= total) return;
@@ -93,23 +118,6 @@ __global__ void __launch_bounds__(256) rq_prep_kernel(const float* __restrict__ 
   const size_t u = ((((size_t)(T / inner_n) * S + s) * inner_n + T % inner_n) * 2) * 64 + lane;
   frag[u] = hi;
   frag[u + 64] = lo;
-}
-
-// |x_r|^2 in fp32 (one wave per row); rows in [R, Rp) get pad_value (+inf for the codebook, so
-// padded rows never rank; 0 for padded queries, whose results are not written).
-__global__ void __launch_bounds__(256) rq_norm_kernel(const float* __restrict__ X, int R, int D, int Rp, float pad_value,
-                                                      float* __restrict__ nrm) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= Rp) return;
-  float s = 0.0f;
-  if (row < R)
-    for (int k = lane; k < D; k += 64) {
-      const float x = X[(size_t)row * D + k];
-      s += x * x;
-    }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) nrm[row] = row < R ? s : pad_value;
 }
 
 __device__ __forceinline__ unsigned long long dist_key(float d, unsigned row) {
@@ -431,16 +439,11 @@ __global__ void __launch_bounds__(256) rq_merge_kernel(const unsigned long long*
 
 // ------------------------------------------------------------------------------------------
 extern "C" hipError_t m3s_launch_rq_prep(const float* X, int R, int D, int S, int ntiles, int inner_n, uint4* frag,
-                                         hipStream_t s) {
+                                         int Rp, float pad_value, float* nrm, hipStream_t s) {
   const size_t total = (size_t)ntiles * S * 64;
-  hipLaunchKernelGGL(m3s::rq_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, R, D, S, ntiles,
-                     inner_n, frag);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t m3s_launch_rq_norm(const float* X, int R, int D, int Rp, float pad_value, float* nrm,
-                                         hipStream_t s) {
-  hipLaunchKernelGGL(m3s::rq_norm_kernel, dim3((Rp + 3) / 4), dim3(256), 0, s, X, R, D, Rp, pad_value, nrm);
+  const int nfrag = (int)((total + 255) / 256);
+  hipLaunchKernelGGL(m3s::rq_prep_kernel, dim3(nfrag + (Rp + 3) / 4), dim3(256), 0, s, X, R, D, S, ntiles, inner_n,
+                     frag, nfrag, Rp, pad_value, nrm);
   return hipGetLastError();
 }
 
