@@ -99,11 +99,14 @@ _SIGS = {
 EXPORTED = sorted(_SIGS)
 
 _LIB = None
+_GPU_OK = False  # a HIP device was verified once: later calls skip the query
 
 
 def load(require_gpu=True):
     """Load libm3s.so. With require_gpu, raise unless a HIP device is visible to torch."""
-    global _LIB
+    global _LIB, _GPU_OK
+    if _LIB is not None and _GPU_OK:  # hot path: every operator call after the first (no device query)
+        return _LIB
     if require_gpu and not torch.cuda.is_available():
         raise RuntimeError("m3s: no HIP device visible; the MI355X kernels have no CPU fallback")
     if _LIB is None:
@@ -117,6 +120,7 @@ def load(require_gpu=True):
         if lib.m3s_abi_version() != ABI_VERSION:
             raise RuntimeError(f"m3s: ABI version mismatch (library {lib.m3s_abi_version()}, bindings {ABI_VERSION})")
         _LIB = lib
+    _GPU_OK = _GPU_OK or require_gpu
     return _LIB
 
 
