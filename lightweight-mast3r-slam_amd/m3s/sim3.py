@@ -209,3 +209,13 @@ class SE3:
 
     def __repr__(self):
         return f"SE3({self.data})"
+
+
+def as_SE3(X):
+    """``lietorch_utils.as_SE3`` (``lietorch_utils.py:6-13``): an SE3 passes through; a Sim3 (any batch shape)
+    becomes a flat (M,) SE3 of its [t, q] on the host, the scale dropped."""
+    if isinstance(X, SE3):
+        return X
+    d = X.data.detach().cpu()
+    t, q, _ = d.reshape(-1, d.shape[-1]).split([3, 4, 1], -1)
+    return SE3(torch.cat([t, q], dim=-1))

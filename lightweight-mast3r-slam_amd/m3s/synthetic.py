@@ -17,6 +17,15 @@ import torch
 import torch.nn.functional as F
 
 
+def tum_fr1_intrinsics(H=384, W=512):
+    """TUM freiburg1 calibration (dataloader.py:78-81, 640x480) scaled to the MASt3R frame like
+    Intrinsics.from_calib's K_frame (dataloader.py:289-293): 640x480 -> 512x384 is a 1.25 downscale, no crop."""
+    s = 640.0 / W
+    assert abs(480.0 / H - s) < 1e-9, "TUM frames keep the 4:3 aspect"
+    fx, fy, cx, cy = 517.3 / s, 516.5 / s, 318.6 / s, 255.3 / s
+    return torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float32)
+
+
 def intrinsics(H, W, device="cpu"):
     f = 0.8 * W
     return torch.tensor([[f, 0.0, W / 2.0], [0.0, f, H / 2.0], [0.0, 0.0, 1.0]], dtype=torch.float32, device=device)
@@ -56,11 +65,11 @@ def quat_from_axis_angle(axis, angle):
 
 
 def make_pair(H=64, W=64, Fd=24, seed=0, flow=(3.3, -2.7), rot_deg=1.0, noise=0.002, desc_noise=0.05,
-              t_gt=(0.01, -0.005, 0.004), rot_gt_deg=0.5, scale_gt=1.01):
+              t_gt=(0.01, -0.005, 0.004), rot_gt_deg=0.5, scale_gt=1.01, K=None):
     """Returns dict with X (2,H,W,3), C (2,H,W), D (2,H,W,F), Q (2,H,W), Xk (H*W,3), Ck (H*W,1),
-    K (3,3), T_gt (8) — all float32 CPU tensors."""
+    K (3,3), T_gt (8) — all float32 CPU tensors. K: camera intrinsics (default `intrinsics(H, W)`)."""
     g = torch.Generator().manual_seed(seed)
-    K = intrinsics(H, W)
+    K = intrinsics(H, W) if K is None else torch.as_tensor(K, dtype=torch.float32)
     fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
     vv, uu = torch.meshgrid(torch.arange(H, dtype=torch.float32), torch.arange(W, dtype=torch.float32), indexing="ij")
     zfun = lambda u, v, gg=g.get_state(): _depth(u, v, H, W, torch.Generator().set_state(gg))
@@ -219,3 +228,124 @@ def retrieval_inputs(seed, C, D, M):
     q = rng.standard_normal((M, D)).astype(np.float32)
     q /= np.linalg.norm(q, axis=1, keepdims=True)
     return c, q
+
+
+# ------------------------------------------------------------------------------------------------
+# C4/C5 factor graphs on a recorded trajectory
+# ------------------------------------------------------------------------------------------------
+def chess_poses(K=256):
+    """The first K of 256 7-Scenes chess ground-truth poses (m3s/data/chess_kf256.txt, written by
+    scripts/make_chess_poses.py from groundtruths/7-scenes/chess.txt), (K,8) float64 [t, q xyzw, s]."""
+    import os
+
+    P = np.loadtxt(os.path.join(os.path.dirname(__file__), "data", "chess_kf256.txt"))
+    assert K <= len(P), f"chess_kf256.txt holds {len(P)} poses"
+    return P[:K]
+
+
+def _act(T, X):
+    """Sim(3) rows T (...,8) acting on points X (...,N,3) (T broadcast over N)."""
+    t, q, s = T[..., None, 0:3], T[..., None, 3:7], T[..., None, 7:8]
+    uv = 2.0 * torch.cross(q[..., :3].expand_as(X), X, dim=-1)
+    return s * (X + q[..., 3:4] * uv + torch.cross(q[..., :3].expand_as(X), uv, dim=-1)) + t
+
+
+def _inv(T):
+    q = torch.cat((-T[..., 3:6], T[..., 6:7]), -1)
+    s = 1.0 / T[..., 7:8]
+    Ti = torch.cat((torch.zeros_like(T[..., :3]), q, s), -1)
+    t = -_act(Ti, T[..., None, 0:3])[..., 0, :]
+    return torch.cat((t, q, s), -1)
+
+
+def _mul(A, B):
+    """Sim(3) composition A * B of rows (...,8)."""
+    qa, qb = A[..., 3:7], B[..., 3:7]
+    xyz = qa[..., 3:4] * qb[..., :3] + qb[..., 3:4] * qa[..., :3] + torch.cross(qa[..., :3], qb[..., :3], dim=-1)
+    w = qa[..., 3:4] * qb[..., 3:4] - (qa[..., :3] * qb[..., :3]).sum(-1, keepdim=True)
+    t = _act(A, B[..., None, 0:3])[..., 0, :]
+    return torch.cat((t, xyz, w, A[..., 7:8] * B[..., 7:8]), -1)
+
+
+def make_traj_graph(poses, H, W, loops_per_kf=3, seed=1, outlier_frac=0.05, valid_prob=0.8,
+                    pose_noise=(0.02, 1.0, 0.01), device="cpu", covis_grid=(12, 16)):
+    """SURVEY.md §8(d) C4/C5 synthetic factor graph on a recorded trajectory (e.g. `chess_poses()`).
+
+    Keyframe k gets the consecutive edge (k-1, k) (main.py:116-120, n_consec = 1) and up to `loops_per_kf`
+    retrieval-like edges (main.py:121-131, retrieval k = 3, base.yaml:53): the earlier keyframes i < k-1 that
+    see most of keyframe k's view (ground-truth co-visibility on a coarse pixel grid, which is what the image
+    retrieval ranks by), kept when at least 5 % of the grid is co-visible. The pointmaps are ray-cast into a
+    box room around the trajectory, the matches are GT reprojections with `outlier_frac` random outliers, and
+    both directions of every edge are built the way FactorGraph.add_factors stores them (global_opt.py:32-101:
+    ii = [i, j], jj = [j, i], idx_ii2jj for each direction). Everything is computed on `device`.
+
+    Returns dict: Twc_gt, Twc0 (K,8) f32 (kf 0 exact), Xs (K,N,3), Cs (K,N,1), ii, jj (E_dir,) i64,
+    idx (E_dir,N) i64, valid (E_dir,N,1) bool, Q (E_dir,N,1) f32, K (3,3), H, W, E_und."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    P = torch.as_tensor(np.asarray(poses), dtype=torch.float64)
+    n_kf = P.shape[0]
+    centre = P[:, :3].mean(0)
+    half = float((P[:, :3] - centre).abs().max()) + 1.5
+    P[:, :3] -= centre  # the room is the box [-half, half]^3 around the trajectory
+    Twc_gt = P.float().to(dev)
+    N = H * W
+    Kc = intrinsics(H, W, device=dev)
+    fx, fy, cx, cy = [float(x) for x in (Kc[0, 0], Kc[1, 1], Kc[0, 2], Kc[1, 2])]
+
+    def rays(h, w):
+        vv, uu = torch.meshgrid(torch.linspace(0, H - 1, h, device=dev), torch.linspace(0, W - 1, w, device=dev),
+                                indexing="ij")
+        return torch.stack(((uu - cx) / fx, (vv - cy) / fy, torch.ones_like(uu)), -1).reshape(-1, 3)
+
+    def pointmaps(rc, Ts):
+        dirs = _act(Ts, rc.expand(Ts.shape[0], -1, -1)) - Ts[:, None, :3]
+        out = []
+        for k in range(Ts.shape[0]):
+            d = _raycast_box(Ts[k, :3], F.normalize(dirs[k], dim=-1), half)
+            out.append(rc * (d / rc.norm(dim=-1))[:, None])
+        return torch.stack(out)
+
+    def project(Tij, Xj):
+        Xi = _act(Tij, Xj)
+        z = Xi[..., 2]
+        return fx * Xi[..., 0] / z + cx, fy * Xi[..., 1] / z + cy, z
+
+    # retrieval-like loop candidates from coarse GT co-visibility
+    Xg = pointmaps(rays(*covis_grid), Twc_gt)
+    edges = [(k - 1, k) for k in range(1, n_kf)]
+    inv_all = _inv(Twc_gt)
+    for k in range(2, n_kf):
+        Tik = _mul(inv_all[: k - 1], Twc_gt[k].expand(k - 1, 8))
+        u, v, z = project(Tik, Xg[k].expand(k - 1, -1, -1))
+        score = ((z > 0.1) & (u >= 0) & (u <= W - 1) & (v >= 0) & (v <= H - 1)).float().mean(1)
+        top = torch.topk(score, min(loops_per_kf, k - 1))
+        edges += [(int(i), k) for s, i in zip(top.values.tolist(), top.indices.tolist()) if s >= 0.05]
+    E_und = len(edges)
+    Xs = pointmaps(rays(H, W), Twc_gt)
+    ii_u = torch.tensor([e[0] for e in edges], dtype=torch.int64, device=dev)
+    jj_u = torch.tensor([e[1] for e in edges], dtype=torch.int64, device=dev)
+    ii = torch.cat((ii_u, jj_u))
+    jj = torch.cat((jj_u, ii_u))
+    E = ii.shape[0]
+    idx = torch.empty(E, N, dtype=torch.int64, device=dev)
+    valid = torch.empty(E, N, 1, dtype=torch.bool, device=dev)
+    for e in range(E):  # idx_ii2jj: for each pixel of j its pixel in i
+        i, j = int(ii[e]), int(jj[e])
+        u, v, z = project(_mul(inv_all[i], Twc_gt[j]), Xs[j])
+        inb = (z > 0.1) & (u >= 0) & (u <= W - 1) & (v >= 0) & (v <= H - 1)
+        lin = u.round().clamp(0, W - 1).long() + W * v.round().clamp(0, H - 1).long()
+        out = torch.rand(N, generator=g, device=dev) < outlier_frac
+        idx[e] = torch.where(out, torch.randint(0, N, (N,), generator=g, device=dev), lin)
+        valid[e, :, 0] = inb & (torch.rand(N, generator=g, device=dev) < valid_prob)
+    Cs = 1.0 + torch.empty(n_kf, N, 1, device=dev).exponential_(0.25, generator=g)
+    Q = 1.0 + torch.empty(E, N, 1, device=dev).exponential_(0.25, generator=g)
+    t_n, r_n, s_n = pose_noise
+    gc = torch.Generator().manual_seed(seed)  # pose noise on the host: identical on every device
+    Twc0 = Twc_gt.cpu().clone()
+    for k in range(1, n_kf):
+        dq = quat_from_axis_angle(torch.randn(3, generator=gc).tolist(), math.radians(r_n) * float(torch.randn(1, generator=gc)))
+        dT = torch.cat((t_n * torch.randn(3, generator=gc), dq, torch.tensor([1.0 + s_n * float(torch.randn(1, generator=gc))])))
+        Twc0[k] = _mul(dT, Twc0[k])
+    return dict(Twc_gt=Twc_gt, Twc0=Twc0.to(dev), Xs=Xs.float(), Cs=Cs, ii=ii, jj=jj, idx=idx, valid=valid, Q=Q,
+                K=Kc, H=H, W=W, E_und=E_und)
