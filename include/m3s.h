@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define M3S_ABI_VERSION 3
+#define M3S_ABI_VERSION 4
 
 #define M3S_OK 0
 #define M3S_EINVAL -1  /* bad shape / argument (reference: TORCH_CHECK -> RuntimeError) */
@@ -110,6 +110,11 @@ int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /* syncs the stream */
+/* Host-only diagnostic of the symbolic factorisation the plan builds for these edges (host arrays):
+ * stats[0] = factor blocks (7x7, diagonal included), [1] = elimination-tree levels, [2] = update groups
+ * (source level, target column), [3] = update sources, [4] = source-map entries, [5] = groups run by
+ * factor tasks. */
+int m3s_ba_pattern_stats(const int64_t* ii, const int64_t* jj, int E, int Kp, int* stats);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused operators (replace stretches of the reference's Python glue)

@@ -5,13 +5,16 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/m3s.h"
 #include "m3s_ba.h"
+#include "ba_pattern.h"
 #include "m3s_track.h"
 
 extern "C" {
@@ -32,7 +35,8 @@ hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, hip
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
-hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, int, float, hipStream_t);
+hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, hipStream_t);
+hipError_t m3s_launch_ba_solve_dense(const BaArgs*, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
 hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, int, float, float*, hipStream_t);
 hipError_t m3s_launch_rq_topk(const uint4*, const float*, const uint4*, const float*, int, int, int, int, int,
@@ -427,7 +431,8 @@ struct BaPlanImpl {
   BaArgs a;
   BaParams p;
   int Kp, N, E, e0, e1;
-  int nblocks, nrhs;
+  int nL;
+  int dense;  // 1: the dense fallback factorisation (ba_dense.hip)
   float delta_thresh;
   size_t edge_sums_off, edge_sums_bytes;
   void* ws;
@@ -440,31 +445,62 @@ int ba_chunks(int N, int E) {
   return std::max(1, std::min(want, cap));
 }
 
-size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* es_off) {
-  const int n = std::max(0, (Kp - 1) * 7);
-  const int nb_max = Kp + E;
-  a->ii_rank = c.take<int>(E);
-  a->jj_rank = c.take<int>(E);
+constexpr int BA_DENSE_MAX_POSES = 1025;  // dense fallback workspace: (2n+1) n doubles, ~0.8 GB at this size
+
+// factor blocks of the densest possible pattern (every pose coupled to every other)
+inline size_t ba_max_blocks(int Kp) {
+  const size_t nb = (size_t)std::max(0, Kp - 1);
+  return nb * (nb + 1) / 2;
+}
+
+// the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
+// symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
+constexpr int BA_BLOB_SECTIONS = 19;
+// update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
+// sparse patterns of larger graphs
+inline size_t ba_max_pairs(int Kp) {
+  const size_t nb = (size_t)std::max(0, Kp - 1);
+  return std::min(nb * nb * nb / 6 + nb * nb + 64, 32 * ba_max_blocks(Kp) + 64);
+}
+size_t ba_blob_capacity(int Kp, int E) {
+  const size_t nb = (size_t)std::max(0, Kp - 1), nLm = ba_max_blocks(Kp);
+  // ranks, perm, col_ptr, rowL, lev_ptr, lev_col, grp_ptr, grp, pull_grp, src, sidx, asm CSR, rhs CSR
+  const size_t ints = 2 * (size_t)E + nb + (nb + 1) + nLm + (nb + 1) + nb + (nb + 2) + 4 * nLm + nb + 4 * nLm +
+                      ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E;
+  return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
+}
+
+size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* es_off, void** blob) {
+  const int nb = std::max(0, Kp - 1);
   a->rec = c.take<float4>((size_t)E * N);  // worst case: a shard packs only its own edges
   a->partials = c.take<double>((size_t)E * chunks * 36);
   *es_off = c.off;
   a->edge_sums = c.take<double>((size_t)E * 36);
-  a->blk_row = c.take<int>(nb_max);
-  a->blk_col = c.take<int>(nb_max);
-  a->blk_ptr = c.take<int>(nb_max + 1);
-  a->blk_ent = c.take<int>((size_t)4 * E);
-  a->rhs_ptr = c.take<int>(Kp + 1);
-  a->rhs_ent = c.take<int>((size_t)2 * E);
-  a->H = c.take<double>((size_t)(2 * n + 1) * std::max(n, 1));  // system, rhs row, carried identity rows
-  a->x = c.take<double>(std::max(n, 1));
-  a->dx = c.take<float>(std::max(n, 1));
+  a->L = c.take<double>(std::max<size_t>(ba_max_blocks(Kp), 1) * 64);
+  a->y = c.take<double>((size_t)std::max(nb, 1) * 8);
+  a->xs = c.take<double>((size_t)std::max(nb, 1) * 8);
+  a->dx = c.take<float>((size_t)std::max(nb, 1) * 7);
+  // the dense fallback's system (graphs up to BA_DENSE_MAX_POSES poses)
+  const size_t n = (size_t)nb * 7;
+  a->H = Kp <= BA_DENSE_MAX_POSES ? c.take<double>(std::max<size_t>((2 * n + 1) * n, 1)) : nullptr;
   a->info = c.take<int>(4);
   a->done = a->info + 1;
   a->iters = a->info + 2;
-  a->Xkf = c.take<const float*>(Kp);
-  a->Ckf = c.take<const float*>(Kp);
-  a->Cscale = c.take<float>(Kp);
+  *blob = c.take<char>(ba_blob_capacity(Kp, E));
   return c.off;
+}
+
+// pinned staging for the plan upload; reused across plans once the previous upload has landed
+struct PlanStage {
+  std::mutex mu;
+  char* buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t landed = nullptr;
+  bool pending = false;
+};
+PlanStage& plan_stage() {
+  static PlanStage st;
+  return st;
 }
 
 }  // namespace
@@ -473,7 +509,31 @@ extern "C" size_t m3s_ba_workspace_size(int Kp, int N, int E) {
   Carver c(nullptr);
   BaArgs a;
   size_t off;
-  return ba_carve(c, Kp, N, E, ba_chunks(N, E), &a, &off);
+  void* blob;
+  return ba_carve(c, Kp, N, E, ba_chunks(N, E), &a, &off, &blob);
+}
+
+extern "C" int m3s_ba_pattern_stats(const int64_t* ii, const int64_t* jj, int E, int Kp, int* stats) {
+  M3S_CHECK(ii && jj && stats && E >= 0 && Kp >= 1, "ba pattern: bad arguments");
+  std::vector<int64_t> u(ii, ii + E);
+  u.insert(u.end(), jj, jj + E);
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  M3S_CHECK((int)u.size() <= Kp, "ba pattern: more unique keyframe ids than poses");
+  std::vector<int> ri(E), rj(E);
+  for (int e = 0; e < E; e++) {
+    ri[e] = (int)(std::lower_bound(u.begin(), u.end(), ii[e]) - u.begin());
+    rj[e] = (int)(std::lower_bound(u.begin(), u.end(), jj[e]) - u.begin());
+  }
+  BaPattern P;
+  ba_build_pattern(ri.data(), rj.data(), E, Kp, &P);
+  stats[0] = P.nL;
+  stats[1] = P.nlev;
+  stats[2] = (int)P.grp.size() / 4;
+  stats[3] = (int)P.src.size() / 4;
+  stats[4] = (int)P.sidx.size();
+  stats[5] = (int)std::count_if(P.pull_grp.begin(), P.pull_grp.end(), [](int g) { return g >= 0; });
+  return M3S_OK;
 }
 
 namespace {
@@ -486,7 +546,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
   M3S_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "ba: bad shard range");
-  M3S_CHECK((int64_t)(Kp - 1) * 7 <= 8192, "ba: at most 1171 poses");
+  M3S_CHECK(Kp <= 32768, "ba: at most 32768 poses");
   if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
                                 "ba calib: height*width must equal the points per keyframe");
   if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");
@@ -495,7 +555,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   memset(&P, 0, sizeof(P));
   const int chunks = ba_chunks(N, E);
   Carver c(workspace);
-  ba_carve(c, Kp, N, E, chunks, &P.a, &P.edge_sums_off);
+  void* blob;
+  ba_carve(c, Kp, N, E, chunks, &P.a, &P.edge_sums_off, &blob);
   P.edge_sums_bytes = (size_t)E * 36 * sizeof(double);
   // rank remap (gn_kernels.cu:161-170): unique(cat(ii,jj)) sorted; searchsorted; pin = 1 for rows
   std::vector<int64_t> hii(E), hjj(E);
@@ -514,52 +575,80 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     ri[e] = (int)(std::lower_bound(u.begin(), u.end(), hii[e]) - u.begin());
     rj[e] = (int)(std::lower_bound(u.begin(), u.end(), hjj[e]) - u.begin());
   }
-  // assembly pattern (SparseBlock::update_lhs/rhs, gn_kernels.cu:71-113), lower blocks only,
-  // contributions in edge order. Off-diagonal blocks carry -M (H_ij = -H_jj), diagonal +M.
-  const int nopt = Kp - 1;
-  std::map<std::pair<int, int>, std::vector<int>> blocks;
-  std::vector<std::vector<int>> rhs(std::max(nopt, 0));
-  for (int e = 0; e < E; e++) {
-    const int io = ri[e] - 1, jo = rj[e] - 1;
-    const int rows[4] = {io, io, jo, jo}, cols[4] = {io, jo, io, jo};
-    const int neg[4] = {0, 1, 1, 0};
-    for (int k = 0; k < 4; k++) {
-      if (rows[k] < 0 || cols[k] < 0 || rows[k] < cols[k]) continue;
-      blocks[{rows[k], cols[k]}].push_back(e * 2 + neg[k]);
-    }
-    if (io >= 0) rhs[io].push_back(e * 2 + 1);  // g_i = -g_j
-    if (jo >= 0) rhs[jo].push_back(e * 2 + 0);
-  }
-  std::vector<int> brow, bcol, bptr{0}, bent, rptr{0}, rent;
-  for (auto& kv : blocks) {
-    brow.push_back(kv.first.first);
-    bcol.push_back(kv.first.second);
-    bent.insert(bent.end(), kv.second.begin(), kv.second.end());
-    bptr.push_back((int)bent.size());
-  }
-  for (int r = 0; r < nopt; r++) {
-    rent.insert(rent.end(), rhs[r].begin(), rhs[r].end());
-    rptr.push_back((int)rent.size());
-  }
-  auto h2d = [&](const void* dst, const void* src, size_t bytes) -> hipError_t {
-    if (bytes == 0) return hipSuccess;
-    return hipMemcpyAsync(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice, s);
+  // symbolic factorisation of the pose system (SparseBlock's pattern, gn_kernels.cu:71-113)
+  BaPattern S;
+  ba_build_pattern(ri.data(), rj.data(), E, Kp, &S);
+  // pack every table into one staging image of the device blob
+  struct Sec {
+    const void* src;
+    size_t bytes;
+    const void** dst;
   };
-  // shard-local rank arrays
-  HIP_TRY(h2d(P.a.ii_rank, ri.data() + e0, sizeof(int) * (e1 - e0)), "ba upload");
-  HIP_TRY(h2d(P.a.jj_rank, rj.data() + e0, sizeof(int) * (e1 - e0)), "ba upload");
-  HIP_TRY(h2d(P.a.blk_row, brow.data(), sizeof(int) * brow.size()), "ba upload");
-  HIP_TRY(h2d(P.a.blk_col, bcol.data(), sizeof(int) * bcol.size()), "ba upload");
-  HIP_TRY(h2d(P.a.blk_ptr, bptr.data(), sizeof(int) * bptr.size()), "ba upload");
-  HIP_TRY(h2d(P.a.blk_ent, bent.data(), sizeof(int) * bent.size()), "ba upload");
-  HIP_TRY(h2d(P.a.rhs_ptr, rptr.data(), sizeof(int) * rptr.size()), "ba upload");
-  HIP_TRY(h2d(P.a.rhs_ent, rent.data(), sizeof(int) * rent.size()), "ba upload");
-  HIP_TRY(h2d(P.a.Xkf, Xh, sizeof(const float*) * Kp), "ba upload");
-  HIP_TRY(h2d(P.a.Ckf, Ch, sizeof(const float*) * Kp), "ba upload");
-  HIP_TRY(h2d(P.a.Cscale, scale_h, sizeof(float) * Kp), "ba upload");
+  const Sec secs[] = {
+      {ri.data() + e0, sizeof(int) * (e1 - e0), (const void**)&P.a.ii_rank},
+      {rj.data() + e0, sizeof(int) * (e1 - e0), (const void**)&P.a.jj_rank},
+      {Xh, sizeof(const float*) * Kp, (const void**)&P.a.Xkf},
+      {Ch, sizeof(const float*) * Kp, (const void**)&P.a.Ckf},
+      {scale_h, sizeof(float) * Kp, (const void**)&P.a.Cscale},
+      {S.perm.data(), sizeof(int) * S.perm.size(), (const void**)&P.a.perm},
+      {S.col_ptr.data(), sizeof(int) * S.col_ptr.size(), (const void**)&P.a.col_ptr},
+      {S.rowL.data(), sizeof(int) * S.rowL.size(), (const void**)&P.a.rowL},
+      {S.lev_ptr.data(), sizeof(int) * S.lev_ptr.size(), (const void**)&P.a.lev_ptr},
+      {S.lev_col.data(), sizeof(int) * S.lev_col.size(), (const void**)&P.a.lev_col},
+      {S.grp_ptr.data(), sizeof(int) * S.grp_ptr.size(), (const void**)&P.a.grp_ptr},
+      {S.grp.data(), sizeof(int) * S.grp.size(), (const void**)&P.a.grp},
+      {S.pull_grp.data(), sizeof(int) * S.pull_grp.size(), (const void**)&P.a.pull_grp},
+      {S.src.data(), sizeof(int) * S.src.size(), (const void**)&P.a.src},
+      {S.sidx.data(), sizeof(int) * S.sidx.size(), (const void**)&P.a.sidx},
+      {S.asm_ptr.data(), sizeof(int) * S.asm_ptr.size(), (const void**)&P.a.asm_ptr},
+      {S.asm_ent.data(), sizeof(int) * S.asm_ent.size(), (const void**)&P.a.asm_ent},
+      {S.rhs_ptr.data(), sizeof(int) * S.rhs_ptr.size(), (const void**)&P.a.rhs_ptr},
+      {S.rhs_ent.data(), sizeof(int) * S.rhs_ent.size(), (const void**)&P.a.rhs_ent},
+  };
+  static_assert(sizeof(secs) / sizeof(secs[0]) == BA_BLOB_SECTIONS, "blob sections");
+  size_t total = 0;
+  for (const Sec& x : secs) total += (x.bytes + 15) & ~(size_t)15;
+  if (S.sidx.size() > ba_max_pairs(Kp) || total > ba_blob_capacity(Kp, E))
+    return fail(M3S_EINVAL, "ba: factor pattern too dense for the plan tables");
+  {
+    PlanStage& st = plan_stage();
+    std::lock_guard<std::mutex> lock(st.mu);
+    if (st.pending) HIP_TRY(hipEventSynchronize(st.landed), "ba stage wait");
+    st.pending = false;
+    if (!st.landed) HIP_TRY(hipEventCreateWithFlags(&st.landed, hipEventDisableTiming), "ba stage event");
+    if (st.cap < total) {
+      if (st.buf) (void)hipHostFree(st.buf);
+      st.buf = nullptr;
+      st.cap = 0;
+      const size_t want = std::max(total, (size_t)1 << 20);
+      HIP_TRY(hipHostMalloc((void**)&st.buf, want, hipHostMallocDefault), "ba stage alloc");
+      st.cap = want;
+    }
+    size_t off = 0;
+    for (const Sec& x : secs) {
+      if (x.bytes) memcpy(st.buf + off, x.src, x.bytes);
+      *x.dst = static_cast<char*>(blob) + off;
+      off += (x.bytes + 15) & ~(size_t)15;
+    }
+    if (total) HIP_TRY(hipMemcpyAsync(blob, st.buf, total, hipMemcpyHostToDevice, s), "ba upload");
+    HIP_TRY(hipEventRecord(st.landed, s), "ba stage record");
+    st.pending = true;
+  }
   HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
   HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");
-  HIP_TRY(hipStreamSynchronize(s), "ba upload sync");  // host vectors die at return
+  // sparse or dense factorisation: measured on MI355X (scripts/ba_exp.py), the one-workgroup sparse
+  // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
+  // update volume); the dense one ~2.7 us per pose (its pivot chain)
+  P.dense = P.a.H != nullptr && 3.8 * S.nlev + 0.03 * (double)S.sidx.size() > 2.7 * S.nb;
+  if (const char* f = getenv("M3S_BA_SOLVER")) {  // tests and experiments: force one factorisation
+    if (!strcmp(f, "sparse")) P.dense = 0;
+    if (!strcmp(f, "dense") && P.a.H) P.dense = 1;
+  }
+  P.a.plan_lo = reinterpret_cast<const char*>(P.a.col_ptr);
+  P.a.plan_bytes = (int)(reinterpret_cast<const char*>(P.a.sidx) + S.sidx.size() * sizeof(int) - P.a.plan_lo);
+  P.a.nb = S.nb;
+  P.a.nlev = S.nlev;
+  P.nL = S.nL;
   P.a.Twc = Twc;
   P.a.idx = idx;
   P.a.valid = valid;
@@ -586,8 +675,6 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.E = E;
   P.e0 = e0;
   P.e1 = e1;
-  P.nblocks = (int)brow.size();
-  P.nrhs = nopt;
   P.delta_thresh = delta_thresh;
   P.ws = workspace;
   P.a.dx = dx_out ? dx_out : P.a.dx;
@@ -653,7 +740,8 @@ extern "C" int m3s_ba_solve(const m3s_ba_plan* plan, void* stream) {
   M3S_CHECK(plan, "ba: null plan");
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
   Span sp("ba_solve", (hipStream_t)stream);
-  HIP_TRY(m3s_launch_ba_solve(&P->a, P->Kp, P->nblocks, P->nrhs, P->delta_thresh, (hipStream_t)stream),
+  HIP_TRY(P->dense ? m3s_launch_ba_solve_dense(&P->a, P->Kp, P->nL, P->delta_thresh, (hipStream_t)stream)
+                   : m3s_launch_ba_solve(&P->a, P->Kp, P->nL, P->delta_thresh, (hipStream_t)stream),
           "ba solve launch");
   return M3S_OK;
 }

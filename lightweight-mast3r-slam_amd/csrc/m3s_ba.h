@@ -32,16 +32,30 @@ struct BaArgs {
   float4* rec;           // (E_local, N) per-call point records (ba_pack): {Xi | u_t, v_t, z_i ; sqrt-weight}
   double* partials;      // (E_local*chunks, 36)
   double* edge_sums;     // (E, 36) global edge rows; all-reduced across ranks in multi-GPU BA
-  // assembly CSR (host-built once per call)
-  const int* blk_row;  // (nblocks) block row (pose index, pin removed)
-  const int* blk_col;  // (nblocks)
-  const int* blk_ptr;  // (nblocks+1)
-  const int* blk_ent;  // edge*2 + (sign<0)
-  const int* rhs_ptr;  // (K-1+1)
+  // block-sparse pose system (ba_pattern.h; analysed once per plan, factored on the device every iteration)
+  int nb;                 // block columns = poses - 1 (pin)
+  int nlev;               // elimination-tree levels
+  const int* perm;        // (nb) factor column -> pose index (pin removed)
+  const int* col_ptr;     // (nb+1) factor blocks of each column, diagonal first
+  const int* rowL;        // (nL) block row of each factor block
+  const int* lev_ptr;     // (nlev+1) -> lev_col
+  const int* lev_col;     // (nb) columns grouped by level
+  const int* grp_ptr;     // (nlev+2) -> grp: the update groups of each step
+  const int4* grp;        // {target column j, src begin, src end, 0}
+  const int* pull_grp;    // (nb) the group a column's factor task runs first, or -1
+  const int4* src;        // {block of L_jk, k, sidx offset, 0}
+  const int* sidx;        // per group source, per block of column j: the source block of column k, or -1
+  const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, staged into LDS by the factor kernel
+  int plan_bytes;
+  const int* asm_ptr;     // (nL+1) assembly CSR: edge*2 + (sign<0), edge order
+  const int* asm_ent;
+  const int* rhs_ptr;     // (nb+1) per factor row
   const int* rhs_ent;
-  double* H;   // ((2n+1), n), n = 7(K-1); row n = rhs, rows n+1.. = carried identity (-> L^-T)
-  double* x;   // (n)
-  float* dx;   // (n) output, reference return value
+  double* L;   // (nL, 8, 8) factor blocks (7x7 used; diagonal blocks keep 1/L_mm in column 7)
+  double* y;   // (nb, 8) rhs -> forward-substituted
+  double* xs;  // (nb, 8) solution in factor order
+  float* dx;   // (nb, 7) output in pose order, reference return value
+  double* H;   // dense fallback ((2n+1), n), n = 7 nb: system, rhs row, carried identity (ba_dense.hip)
   int* info;   // factorisation failure flag
   int* done;   // early-exit flag (|dx| < delta_thresh)
   int* iters;  // iterations executed

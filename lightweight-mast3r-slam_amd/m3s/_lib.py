@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # M3S_LIB: alternative build of the same library (kernel experiments); still the HIP library, no fallback
 LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libm3s.so")
 
-ABI_VERSION = 3  # include/m3s.h M3S_ABI_VERSION
+ABI_VERSION = 4  # include/m3s.h M3S_ABI_VERSION
 
 c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
 
@@ -84,6 +84,7 @@ _SIGS = {
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_iterations": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), c_void_p], c_int),
+    "m3s_ba_pattern_stats": ([c_void_p, c_void_p, c_int, c_int, ctypes.POINTER(c_int)], c_int),
     "m3s_peak_fma_f32": ([c_void_p, c_int, c_int, c_void_p], c_int),
     "m3s_match_workspace_size": ([c_int] * 4, c_size_t),
     "m3s_match": ([c_void_p] * 7 + [c_int] * 5 + [c_float] * 3 + [c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
@@ -122,6 +123,20 @@ def load(require_gpu=True):
         _LIB = lib
     _GPU_OK = _GPU_OK or require_gpu
     return _LIB
+
+
+def ba_pattern_stats(ii, jj, Kp):
+    """Host-only: (factor blocks, elimination-tree levels, update groups, update sources, source-map
+    entries, factor-task groups) of the
+    symbolic factorisation a BA plan builds for the directed edges ii, jj (int64 host arrays)."""
+    import numpy as np
+
+    lib = load(require_gpu=False)
+    ii = np.ascontiguousarray(ii, dtype=np.int64)
+    jj = np.ascontiguousarray(jj, dtype=np.int64)
+    out = (c_int * 6)()
+    check(lib.m3s_ba_pattern_stats(c_void_p(ii.ctypes.data), c_void_p(jj.ctypes.data), len(ii), int(Kp), out))
+    return tuple(out)
 
 
 def check(rc):

@@ -1,5 +1,5 @@
 """BA experiment: per-iteration linearize / solve time (HIP-event spans in libm3s) on a synthetic graph.
-usage: python scripts/ba_exp.py [K] [H] [W] [iters]"""
+usage: python scripts/ba_exp.py [K] [H] [W] [iters] [graph: circle|chess] [mode: rays|calib]"""
 import ctypes
 import os
 import sys
@@ -13,24 +13,35 @@ import torch  # noqa: E402
 from m3s import _lib  # noqa: E402
 from m3s.config import config  # noqa: E402
 from m3s.dist_ba import HipShard, ba_config, run_sharded  # noqa: E402
-from m3s.synthetic import make_graph  # noqa: E402
+from m3s.synthetic import chess_poses, make_graph, make_traj_graph  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 384
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 512
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+graph = sys.argv[5] if len(sys.argv) > 5 else "circle"
+mode = sys.argv[6] if len(sys.argv) > 6 else "rays"
 dev = torch.device("cuda")
 t0 = time.time()
-G = make_graph(n_kf=K, H=H, W=W, seed=1, device="cpu")
-print(f"graph K={K} {H}x{W} built in {time.time() - t0:.1f}s", flush=True)
-ii = torch.cat((G["ii"], G["jj"])).to(dev)
-jj = torch.cat((G["jj"], G["ii"])).to(dev)
-idx = torch.cat((G["idx"], G["idx"].flip(1))).to(dev).contiguous()
-valid = torch.cat((G["valid"], G["valid"].flip(1)))[..., 0].to(dev).contiguous()
-Q = torch.cat((G["Q"], G["Q"].flip(1)))[..., 0].to(dev).contiguous()
+if graph == "chess":  # the 7-Scenes chess trajectory, built on the GPU
+    G = make_traj_graph(chess_poses(K), H, W, seed=1, device=dev)
+    ii, jj, idx = G["ii"], G["jj"], G["idx"].contiguous()
+    valid, Q = G["valid"][..., 0].contiguous(), G["Q"][..., 0].contiguous()
+else:
+    G = make_graph(n_kf=K, H=H, W=W, seed=1, device="cpu")
+    ii = torch.cat((G["ii"], G["jj"])).to(dev)
+    jj = torch.cat((G["jj"], G["ii"])).to(dev)
+    idx = torch.cat((G["idx"], G["idx"].flip(1))).to(dev).contiguous()
+    valid = torch.cat((G["valid"], G["valid"].flip(1)))[..., 0].to(dev).contiguous()
+    Q = torch.cat((G["Q"], G["Q"].flip(1)))[..., 0].to(dev).contiguous()
+print(f"graph {graph} K={K} {H}x{W} built in {time.time() - t0:.1f}s", flush=True)
 Xs, Cs = G["Xs"].to(dev).contiguous(), G["Cs"][..., 0].to(dev).contiguous()
+if mode == "calib":  # global_opt.py:163-201: the calib solve sees the points constrained to their rays
+    from m3s.geometry import constrain_points_to_ray
+
+    Xs = constrain_points_to_ray((H, W), Xs, G["K"].to(dev)).contiguous()
 E = ii.shape[0]
-cfg = ba_config("rays", config["local_opt"])
+cfg = ba_config(mode, config["local_opt"], K=G["K"], height=H, width=W)
 lib = _lib.load()
 for rep in range(2):
     Twc = G["Twc0"].to(dev).contiguous()
@@ -52,16 +63,16 @@ for rep in range(2):
     print(f"rep {rep}: E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
           f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}", flush=True)
 
-if hasattr(lib, "m3s_debug_chol_stamps"):
-    buf = (ctypes.c_ulonglong * 1024)()
-    lib.m3s_debug_chol_stamps(buf)
-    n = (K - 1) * 7
-    npan = min(64, (n + 63) // 64)
-    names = {1: "loaded", 2: "diag look-ahead", 3: "L0", 4: "L1", 5: "L2", 6: "L3", 7: "chain end", 8: "X look-ahead",
-             9: "T0", 10: "T1", 11: "T2", 12: "T3", 13: "synced", 14: "stored"}
-    for sel in (range(1, 2), range(npan // 2, npan // 2 + 1), range(npan - 1, npan)):
-        for p in sel:
-            t0 = buf[p * 16]
-            print(f"panel {p}: " + "  ".join(f"{nm}={(buf[p * 16 + k] - t0) / 100.0:.2f}" for k, nm in names.items()))
-    gaps = [(buf[(p + 1) * 16] - buf[p * 16 + 14]) / 100.0 for p in range(npan - 1)]
-    print(f"gap from panel-block-0 end to next launch's block-0 start: mean {sum(gaps) / len(gaps):.2f} us")
+
+if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the last factor launch
+    buf = (ctypes.c_ulonglong * 4096)()
+    lib.m3s_debug_sp_stamps(buf)
+    st = _lib.ba_pattern_stats(ii.cpu().numpy(), jj.cpu().numpy(), Xs.shape[0])
+    nlev = st[1]
+    t = [(buf[k] - buf[0]) / 100.0 for k in range(5 + 2 * nlev)]  # us (100 MHz)
+    steps = [t[2 + l] - t[1 + l] for l in range(nlev + 1)]
+    print(f"factor stamps: nlev {nlev} blocks {st[0]} groups {st[2]} sources {st[3]} sidx {st[4]} "
+          f"pull groups {st[5]}: prologue {t[1]:.1f} us, factor {t[2 + nlev] - t[1]:.1f} us, "
+          f"back {t[3 + 2 * nlev] - t[2 + nlev]:.1f} us, tail {t[4 + 2 * nlev] - t[3 + 2 * nlev]:.1f} us, "
+          f"total {t[4 + 2 * nlev]:.1f}")
+    print("steps:", " ".join(f"{x:.2f}" for x in steps))

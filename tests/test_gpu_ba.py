@@ -204,10 +204,14 @@ def _host_solve_from_edge_sums(es, ii, jj):
     return -np.linalg.solve(Hs, g)
 
 
+@pytest.mark.parametrize("solver", ["sparse", "dense"])
 @pytest.mark.parametrize("n_kf", [48, 97])
-def test_dense_solve_matches_lapack_on_large_graph(n_kf):
-    """The device factorisation (panels, look-ahead trailing tiles, carried inverse rows, ragged last
-    panel) against LAPACK on the same assembled system: one GN step from the device's own edge sums."""
+def test_pose_solve_matches_lapack_on_large_graph(n_kf, solver, monkeypatch):
+    """Both device factorisations against LAPACK on the same assembled system, one GN step from the
+    device's own edge sums: the block-sparse one (elimination-tree levels, update groups, columns of
+    more than 128 rows on these fill-heavy random-loop graphs) and the dense fallback (panels,
+    look-ahead trailing tiles, carried inverse rows, ragged last panel)."""
+    monkeypatch.setenv("M3S_BA_SOLVER", solver)
     from m3s.config import config
     from m3s.dist_ba import HipShard, ba_config
     from m3s.synthetic import make_graph, two_way

@@ -132,11 +132,15 @@ def chess_graph():
     return {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in G.items()}
 
 
+@pytest.mark.parametrize("solver", ["auto", "dense"])
 @pytest.mark.parametrize("mode", ["rays", "calib"])
-def test_ba_k256_chess_graph_vs_fp64_truth(chess_graph, mode):
-    """C4/C5-shaped global BA: 256 keyframes (255 optimised poses, n = 1785), ~2000 directed edges."""
+def test_ba_k256_chess_graph_vs_fp64_truth(chess_graph, mode, solver, monkeypatch):
+    """C4/C5-shaped global BA: 256 keyframes (255 optimised poses, n = 1785), ~2000 directed edges; the
+    plan's own choice of factorisation (block-sparse on this graph) and the dense fallback."""
     import mast3r_slam_backends as B
 
+    if solver != "auto":
+        monkeypatch.setenv("M3S_BA_SOLVER", solver)
     G = chess_graph
     H, W = G["H"], G["W"]
     Xs = G["Xs"] if mode == "rays" else O.backproject_constrain(G["Xs"], G["K"], (H, W))

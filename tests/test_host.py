@@ -212,3 +212,73 @@ def test_retrieval_abi_validates_before_any_launch():
     assert rc != 0 and b"too small" in lib.m3s_last_error()
     rc = lib.m3s_quantize(q(0), 100, 64, p, 5, 5, p, p, ctypes.c_size_t(1 << 30), q(0))
     assert rc != 0 and b"null" in lib.m3s_last_error()
+
+
+def _min_degree_symbolic(ii, jj, Kp):
+    """Independent restatement of the plan's symbolic analysis (ba_pattern.cpp): minimum-degree
+    elimination on the pose graph (pin removed, ties to the lowest index), the factor's block count,
+    its elimination-tree height, and the update groups: one per (source level, target column), the
+    group of a column's children's level run by its own factor task."""
+    u = np.unique(np.concatenate([ii, jj]))
+    ri, rj = np.searchsorted(u, ii) - 1, np.searchsorted(u, jj) - 1
+    nb = Kp - 1
+    adj = [set() for _ in range(nb)]
+    for a, b in zip(ri, rj):
+        if a >= 0 and b >= 0 and a != b:
+            adj[a].add(b)
+            adj[b].add(a)
+    alive, order, struct = set(range(nb)), [], {}
+    while alive:
+        v = min(alive, key=lambda x: (len(adj[x]), x))
+        order.append(v)
+        alive.remove(v)
+        nv = set(adj[v])
+        struct[v] = nv
+        for a in nv:
+            adj[a] |= nv
+            adj[a] -= {a, v}
+        adj[v] = set()
+    pos = {v: k for k, v in enumerate(order)}
+    S = [sorted(pos[a] for a in struct[order[j]]) for j in range(nb)]
+    lev = [0] * nb
+    for j in range(nb):
+        if S[j]:
+            lev[S[j][0]] = max(lev[S[j][0]], lev[j] + 1)
+    nlev = max(lev) + 1 if nb else 0
+    pairs_kj = [(k, j) for k in range(nb) for j in S[k]]
+    groups = len({(lev[k], j) for k, j in pairs_kj})
+    sidx = sum(len(S[j]) + 1 for k, j in pairs_kj)
+    pulls = len({j for k, j in pairs_kj if lev[k] == lev[j] - 1})
+    return nb + len(pairs_kj), nlev, groups, len(pairs_kj), sidx, pulls
+
+
+@pytest.mark.parametrize("kind", ["chain", "loops", "chess"])
+def test_ba_symbolic_factorisation_matches_restatement(kind):
+    """The BA plan's block-sparse pattern (SparseBlock's system, gn_kernels.cu:57-159) against an
+    independent Python elimination: identical fill, elimination-tree height and update lists."""
+    from m3s import _lib
+
+    if kind == "chain":  # consecutive edges only: tridiagonal, no fill
+        K = 40
+        und = [(k - 1, k) for k in range(1, K)]
+    elif kind == "loops":
+        K, g = 60, np.random.default_rng(3)
+        und = [(k - 1, k) for k in range(1, K)] + [(int(c), k) for k in range(4, K)
+                                                   for c in g.choice(k - 1, 3, replace=False)]
+    else:  # the K=256 chess trajectory's loop-closure graph used by the BA bench and config tests
+        from m3s.synthetic import chess_poses, make_traj_graph
+
+        G = make_traj_graph(chess_poses(256), 12, 16, covis_grid=(12, 16))
+        K = 256
+        und = list(zip(G["ii"][: G["E_und"]].tolist(), G["jj"][: G["E_und"]].tolist()))
+    ii = np.array([a for a, b in und] + [b for a, b in und], dtype=np.int64) * 3 + 7  # global ids, remapped
+    jj = np.array([b for a, b in und] + [a for a, b in und], dtype=np.int64) * 3 + 7
+    got = _lib.ba_pattern_stats(ii, jj, K)
+    want = _min_degree_symbolic(ii, jj, K)
+    assert got == want
+    nb = K - 1
+    assert got[0] <= nb * (nb + 1) // 2
+    if kind == "chain":
+        assert got[0] == 2 * nb - 1
+    if kind == "chess":  # the point of the sparse solve: little fill, a short elimination tree
+        assert got[0] < 0.1 * nb * (nb + 1) // 2 and got[1] < nb // 2
