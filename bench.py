@@ -14,6 +14,8 @@ synthetic factor graph's edges over the ranks (strong scaling, one RCCL all-redu
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import ctypes
+import platform
 import glob
 import json
 import os
@@ -46,9 +48,7 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--mode", choices=["calib", "rays"], default="calib")
     ap.add_argument("--ring", type=int, default=6, help="distinct synthetic pairs cycled (ring > L3)")
-    ap.add_argument("--ba-kf", type=int, default=256)  # C5: 256-keyframe synthetic factor graph
-    ap.add_argument("--ba-h", type=int, default=384)
-    ap.add_argument("--ba-w", type=int, default=512)
+    ap.add_argument("--ba-kf", type=int, default=256)  # C4/C5: 256-keyframe factor graphs (BA_LEGS)
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured HBM-copy / FMA peak probes")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP-event spans inside the timed loop (no roofline)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
 
@@ -163,10 +163,10 @@ KERNEL_SYMBOL = {"prep_rays": "prep_rays_kernel", "proj_occlusion": "proj_occlus
                  "refine_lin": "refine_tile_kernel", "track_setup": "track_setup_kernel", "gn_iters": "gn_iter_kernel"}
 
 
-def pmc_traffic(name):
+def pmc_traffic(name, pattern="r[0-9][0-9]_pmc.json"):
     """HBM bytes per launch of `name` from the newest committed rocprofv3 PMC summary
     (profiles/<round>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, scripts/profile_summary.py); None if absent."""
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r[0-9][0-9]_pmc.json")))
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", pattern)))
     if not files:
         return None
     for k, v in json.load(open(files[-1])).items():
@@ -175,44 +175,119 @@ def pmc_traffic(name):
     return None
 
 
-def bench_ba(args, rank, world, dev):
+# SURVEY.md §8(d) BA legs: C5 = 256-keyframe chess graph, calib, 512x384 (7-Scenes shape); C4 = EuRoC-shaped
+# graph (MH_02_easy trajectory), rays (eval_no_calib), 512x320
+BA_LEGS = {"C5": dict(traj="chess", mode="calib", H=384, W=512), "C4": dict(traj="euroc", mode="rays", H=320, W=512)}
+BA_BYTES_PER_POINT = 45  # Xi gather 12 + idx 8 + valid 1 + Xj 12 + Q 4 + Ci 4 + Cj 4
+BA_BYTES_PER_EDGE = 840  # Hs / gs out
+
+
+def bench_ba(args, rank, world, dev, leg):
+    from m3s import _lib
     from m3s.config import config
     from m3s.dist_ba import HipShard, ba_config, run_sharded, shard_range
-    from m3s.synthetic import make_graph
+    from m3s.geometry import constrain_points_to_ray
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
 
-    G = make_graph(n_kf=args.ba_kf, H=args.ba_h, W=args.ba_w, seed=1, device="cpu")
-    # two-way edges; the reverse maps are a cheap permutation of the forward ones for throughput purposes
-    ii = torch.cat((G["ii"], G["jj"])).to(dev)
-    jj = torch.cat((G["jj"], G["ii"])).to(dev)
-    idx = torch.cat((G["idx"], G["idx"].flip(1))).to(dev).contiguous()
-    valid = torch.cat((G["valid"], G["valid"].flip(1)))[..., 0].to(dev).contiguous()
-    Q = torch.cat((G["Q"], G["Q"].flip(1)))[..., 0].to(dev).contiguous()
-    Xs, Cs = G["Xs"].to(dev).contiguous(), G["Cs"][..., 0].to(dev).contiguous()
+    L = BA_LEGS[leg]
+    H, W, mode = L["H"], L["W"], L["mode"]
+    poses = (chess_poses if L["traj"] == "chess" else euroc_poses)(args.ba_kf)
+    G = make_traj_graph(poses, H, W, seed=1, device=dev)  # same seed on every rank: identical graphs
+    ii, jj, idx = G["ii"], G["jj"], G["idx"].contiguous()
+    valid, Q = G["valid"][..., 0].contiguous(), G["Q"][..., 0].contiguous()
+    Xs, Cs = G["Xs"].contiguous(), G["Cs"][..., 0].contiguous()
+    if mode == "calib":  # global_opt.py:163-201: the calib solve sees the points constrained to their rays
+        Xs = constrain_points_to_ray((H, W), Xs, G["K"]).contiguous()
     E = ii.shape[0]
+    N = H * W
     e0, e1 = shard_range(E, rank, world)
-    cfg = ba_config("rays", config["local_opt"])
+    cfg = ba_config(mode, config["local_opt"], K=G["K"], height=H, width=W)
+    lib = _lib.load()
 
-    def run(iters):
-        # the whole gauss_newton call is timed: plan (rank remap, assembly pattern, per-call
+    def run(iters, timed_kernels=False):
+        # the whole gauss_newton call is timed: plan (rank remap, symbolic factorisation, per-call
         # point records of this rank's edges) + iters x (linearise, all-reduce, solve, retract)
         Twc = G["Twc0"].to(dev).contiguous()
         sync_all(world)
+        if timed_kernels:
+            lib.m3s_timing_reset()
+            lib.m3s_timing_enable(1)
         t0 = time.perf_counter()
         shard = HipShard(cfg, Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.0, e0, e1)  # delta 0: no early exit
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         run_sharded(shard, iters)
         sync_all(world)
-        return time.perf_counter() - t0, t1 - t0
+        el = time.perf_counter() - t0
+        spans = {}
+        if timed_kernels:
+            lib.m3s_timing_enable(0)
+            for name in ("ba_linearize", "ba_solve"):
+                ms, cnt = ctypes.c_double(), ctypes.c_int()
+                _lib.check(lib.m3s_timing_query(name.encode(), ms, cnt))
+                spans[name] = ms.value / max(cnt.value, 1)
+        return el, t1 - t0, spans
 
     run(1)  # warmup
-    el, setup = run(args.ba_iters)
+    el, setup, _ = run(args.ba_iters)
     el = max_over_ranks(el, world)
     setup = max_over_ranks(setup, world)
-    return {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
-            "points_per_kf": args.ba_h * args.ba_w, "iters": args.ba_iters, "ms_per_call": el * 1e3,
-            "ms_setup": setup * 1e3, "ms_per_iter": (el - setup) / args.ba_iters * 1e3,
-            "scaling": "strong", "mode": "rays"}
+    _, _, spans = run(args.ba_iters, timed_kernels=True)  # HIP-event spans, a second pass (events cost host time)
+    st = _lib.ba_pattern_stats(ii.cpu().numpy(), jj.cpu().numpy(), args.ba_kf)
+    # roofline of the dominant kernel (the linearisation) at SURVEY §8(d)'s algorithmic bytes per edge-iteration
+    lin_s = spans["ba_linearize"] * 1e-3
+    alg = (e1 - e0) * (BA_BYTES_PER_POINT * N + BA_BYTES_PER_EDGE)
+    traffic = pmc_traffic("ba_lin_kernel", pattern="r[0-9][0-9]_ba_pmc.json")
+    roof = {"kernel": "ba_lin_kernel + ba_edge_kernel", "bound": "hbm", "achieved": alg / lin_s / 1e9,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / lin_s / 1e9 / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_over_alg": (traffic / alg) if traffic else None,
+            "avg_us": spans["ba_linearize"] * 1e3,
+            "alg_bytes": f"{BA_BYTES_PER_POINT} B/point x {N} points + {BA_BYTES_PER_EDGE} B per edge-iteration "
+                         f"(SURVEY.md 8d), x {e1 - e0} edges per launch"}
+    out = {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
+           "points_per_kf": N, "shape": [H, W], "mode": mode, "trajectory": L["traj"], "iters": args.ba_iters,
+           "ms_per_call": el * 1e3, "ms_setup": setup * 1e3, "ms_per_iter": (el - setup) / args.ba_iters * 1e3,
+           "ms_lin_per_iter": spans["ba_linearize"], "ms_solve_per_iter": spans["ba_solve"],
+           "factor": {"blocks": st[0], "levels": st[1], "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2},
+           "scaling": "strong", "roofline": roof}
+    del G, idx, valid, Q, Xs, Cs
+    torch.cuda.empty_cache()
+    return out
+
+
+def ba_cpu_baseline(args, leg="C5", n_kf=8, iters=2):
+    """The oracle's gauss_newton (C restatement of gn_kernels.cu, OpenMP over points) on a bounded sample of
+    the same workload: the first n_kf keyframes of the leg's trajectory at its full shape."""
+    import oracle.oracle as O
+    from m3s.config import config
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
+
+    L = BA_LEGS[leg]
+    H, W, mode = L["H"], L["W"], L["mode"]
+    G = make_traj_graph((chess_poses if L["traj"] == "chess" else euroc_poses)(n_kf), H, W, seed=1, device="cpu")
+    Xs = G["Xs"].numpy()
+    K = G["K"].numpy()
+    if mode == "calib":
+        Xs = O.backproject_constrain(Xs, K, (H, W))
+    c = config["local_opt"]
+    sa, sb = (c["sigma_pixel"], c["sigma_depth"]) if mode == "calib" else (c["sigma_ray"], c["sigma_dist"])
+    p = O.ba_params(mode, sa, sb, c["C_conf"], c["Q_conf"], K=K, height=H, width=W, pixel_border=c["pixel_border"],
+                    z_eps=c["depth_eps"])
+    E = G["ii"].shape[0]
+    out = {}
+    for label, threads, its in (("all_cores", min(16, len(os.sched_getaffinity(0))), iters), ("one_thread", 1, 1)):
+        O.set_threads(threads)
+        t0 = time.perf_counter()
+        O.gauss_newton(mode, G["Twc0"].numpy(), Xs, G["Cs"].numpy()[..., 0], G["ii"].numpy(), G["jj"].numpy(),
+                       G["idx"].numpy(), G["valid"].numpy()[..., 0], G["Q"].numpy()[..., 0], p, its, 0.0)
+        el = time.perf_counter() - t0
+        out[label] = {"value": E * its / el, "cores": threads, "seconds": el}
+    O.set_threads(min(16, len(os.sched_getaffinity(0))))
+    return {"value": out["all_cores"]["value"], "unit": "edges/s", "cores": out["all_cores"]["cores"], "kind": "port",
+            "one_thread": out["one_thread"]["value"],
+            "sample": f"{leg} shape ({H}x{W}, {mode}), first {n_kf} keyframes ({E} directed edges) through the oracle's "
+                      f"gauss_newton (C, OpenMP): {iters} iterations on all cores in {out['all_cores']['seconds']:.1f}s, "
+                      f"1 on one thread in {out['one_thread']['seconds']:.1f}s"}
 
 
 def bench_retrieval(dev):
@@ -321,22 +396,31 @@ def frame_roofline(step_s, N, gn_iters_mean, mode):
             "note": "host-stamped per-frame wall (track() returns after its readback), ViT excluded"}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args):
-    """Oracle (C restatement + numpy glue) on the host cores, bounded sample of the same workload."""
+    """Oracle (C restatement + numpy glue) on the host cores, bounded sample of the same workload: frames on
+    all cores (up to 16, the box's share) for ~cpu_seconds, then one frame on one thread."""
     import oracle.oracle as O
     from m3s.synthetic import make_pair
 
-    cores = min(16, len(os.sched_getaffinity(0)))
-    os.environ["OMP_NUM_THREADS"] = str(cores)
+    avail = len(os.sched_getaffinity(0))
+    cores = min(16, avail)
     H, W = args.height, args.width
     P = make_pair(H, W, seed=0)
     X, C, D, Q = (P[k].numpy() for k in ("X", "C", "D", "Q"))
     Xk, K = P["Xk"].numpy(), P["K"].numpy()
-    N = H * W
-    t0 = time.perf_counter()
-    frames = 0
     I = np.array([0, 0, 0, 0, 0, 0, 1, 1.0])
-    while True:
+
+    def frame():
         idx, valid = O.match(X[:1], X[1:], D[:1], D[1:])
         i = idx[0]
         Qk = np.sqrt(Q[0].reshape(-1)[i] * Q[1].reshape(-1))
@@ -350,13 +434,25 @@ def cpu_baseline(args):
             O.track_calib(Xf, Xk, I, I, Qk, v, meas, vm, K, (H, W))
         else:
             O.track_rays(X[0].reshape(-1, 3)[i], Xk, I, I, Qk, v)
+
+    O.set_threads(cores)
+    t0 = time.perf_counter()
+    frames = 0
+    while True:
+        frame()
         frames += 1
         if time.perf_counter() - t0 > args.cpu_seconds or frames >= 50:
             break
     el = time.perf_counter() - t0
+    O.set_threads(1)
+    t1 = time.perf_counter()
+    frame()
+    el1 = time.perf_counter() - t1
+    O.set_threads(cores)
     return {"value": frames / el, "unit": "tracked frames/s", "cores": cores, "kind": "port",
-            "sample": f"{frames} tracked frames ({H}x{W}, {args.mode}) through oracle/ (C kernels, OpenMP "
-                      f"{cores} threads, + numpy fp64 glue) in {el:.1f}s"}
+            "one_thread": 1.0 / el1, "affinity_cores": avail, "cpu_model": cpu_model(),
+            "sample": f"{frames} tracked frames ({H}x{W}, {args.mode}) through oracle/ (C kernels, OpenMP {cores} "
+                      f"threads, + numpy fp64 glue) in {el:.1f}s; one frame on one thread in {el1:.1f}s"}
 
 
 def main():
@@ -399,11 +495,14 @@ def main():
     peaks = measured_peaks(dev) if (rank == 0 and not args.no_peaks) else None
     ba = None
     if not args.no_ba:
-        ba = bench_ba(args, rank, world, dev)
+        ba = bench_ba(args, rank, world, dev, "C5")
+        ba["c4"] = bench_ba(args, rank, world, dev, "C4")
     retrieval = bench_retrieval(dev) if (rank == 0 and not args.no_retrieval) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
+        if ba is not None:
+            ba["cpu_baseline"] = ba_cpu_baseline(args)
     if rank == 0:
         rec = {
             "metric": "tracked frames/s (match+GN, 512x512 pointmaps) @1 GPU; BA edges/s @1/2/4/8",

@@ -288,9 +288,9 @@ static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, do
                           unsigned long long** cnt, unsigned** tick) {
   *st = c.take<TrackState>(1);
   *cnt = c.take<unsigned long long>(M3S_TRACK_SHARDS * 16);
-  *tick = c.take<unsigned>((M3S_TRACK_SHARDS + 1) * 32);
+  *tick = c.take<unsigned>(M3S_TRACK_TICK_WORDS);
   *flags = c.take<uint8_t>(((size_t)N + 15) / 16 * 16);
-  *partials = c.take<double>((size_t)track_nparts(N) * 40);
+  *partials = c.take<double>((size_t)64 * 256 * 40);  // GN_SLOTS iterations x up to 256 blocks x GN_PSTRIDE
   *rec = c.take<float>((size_t)N * 8);
   return c.off;
 }
@@ -391,25 +391,18 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     Span sp("track_setup", s);
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
   }
+  (void)first_chunk;  // every GN iteration runs inside one persistent launch (gn_loop_kernel)
   const int nparts = track_nparts(N);
-  int launched = 0, chunk_id = 0;
-  int chunk = std::max(1, std::min(first_chunk, p.max_iters));
   TrackState& hs = *pinned_state();
-  for (;; chunk_id++) {
-    {
-      Span sp("gn_iters", s);
-      HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, chunk, chunk_id, s), "track iterate launch");
-    }
-    launched += chunk;
-    // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
-    // before the readback, it runs only if this batch finished the solve (done_chunk == chunk_id)
-    if (do_fuse || !p.direct)
-      HIP_TRY(m3s_launch_fuse(&a, chunk_id, &fa, p.direct ? 0 : 1, N, s), "track fuse launch");
-    HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
-    HIP_TRY(hipStreamSynchronize(s), "track sync");
-    if (hs.done || launched >= p.max_iters) break;
-    chunk = std::min(8, p.max_iters - launched);
+  {
+    Span sp("gn_iters", s);
+    HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, p.max_iters, 0, s), "track iterate launch");
   }
+  // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
+  // before the readback, it runs only if the solve finished with a pose
+  if (do_fuse || !p.direct) HIP_TRY(m3s_launch_fuse(&a, 0, &fa, p.direct ? 0 : 1, N, s), "track fuse launch");
+  HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
+  HIP_TRY(hipStreamSynchronize(s), "track sync");
   memcpy(result->T_WCf, hs.T_WCf, sizeof(result->T_WCf));
   memcpy(result->T_CkCf, hs.T, sizeof(result->T_CkCf));
   result->cost = hs.last_cost;

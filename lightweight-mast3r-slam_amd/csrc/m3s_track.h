@@ -55,9 +55,24 @@ struct TrackArgs {
   double* partials;            // (nparts, 40) block partial sums (workspace)
   TrackState* state;
   unsigned long long* cnt;     // (8 x 16) setup counters, one 128-B line per XCD shard: (n_valid_kf << 32) | n_valid_opt
-  unsigned* tick;              // (9 x 32) GN arrival tickets: 8 shards + the top counter, one 128-B line each
+  unsigned* tick;              // (11 x 32) GN arrival tickets: 8 shards + the top counter, one 128-B line each,
+                               // then the GnBcast record (two lines)
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
 };
+
+// Per-iteration broadcast of the persistent GN launch: written write-through (sc1) by the block that
+// solved iteration `gen`-1, read with sc1 loads by every block once it sees `gen` (MI355X_MICROARCH.md
+// "Hand-offs measured with sc1 loads": one storing lane, sc1 flag, sc1 loads after the poll matched).
+struct GnBcast {
+  float T[8];       // T_CkCf after the last solved iteration
+  double old_cost;  // that iteration's cost (the next convergence test's old_cost)
+  int iter;         // iterations done
+  int done;         // converged / max iterations / Cholesky failure
+  int status;       // M3S_TRACK_*
+  unsigned gen;     // iterations published
+  int pad[2];
+};
+#define M3S_TRACK_TICK_WORDS ((M3S_TRACK_SHARDS + 1 + 2) * 32)
 
 // keyframe fusion (weighted_pointmap) + the match_info average confidences (frame.py:74-77, 83-84)
 struct FuseArgs {

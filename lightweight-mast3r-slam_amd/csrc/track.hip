@@ -13,13 +13,12 @@
 //   track_init   : zero the state and the unique(idx[valid]) byte map, T_CkCf = T_WCk^-1 T_WCf
 //   track_setup  : gather Xf[idx], Qk = sqrt(Qff[idx] Qkf), validity masks, a 32-byte per-point GN
 //                  record, counts (valid_opt, valid_kf) and the byte map
-//   gn_iter (xI) : ONE launch per GN iteration: every block accumulates the 28 (H upper) + 7 (g)
-//                  + 1 (cost) sums in fp64, publishes them write-through (sc1) and takes an arrival
-//                  ticket; the last-arriving block reduces all partials, solves the 7x7 system in
-//                  fp64, retracts T <- Exp(tau) T, applies the convergence test and, once done,
-//                  writes T_WCf = T_WCk T_CkCf (also to the caller's T_out). Later launches exit at
-//                  their first load. The first launch also popcounts the byte map
-//                  (torch.unique(...).shape[0], tracker.py:106-108).
+//   gn_loop      : ONE persistent launch runs every GN iteration: per iteration every block
+//                  accumulates the 28 (H upper) + 7 (g) + 1 (cost) sums in fp64, publishes them
+//                  write-through (sc1) and takes an arrival ticket; the last-arriving block reduces all
+//                  partials, solves the 7x7 system, retracts T <- Exp(tau) T, applies the convergence
+//                  test, broadcasts the new T (GnBcast) and, once done, writes T_WCf = T_WCk T_CkCf
+//                  (also to the caller's T_out); the other blocks poll the broadcast and go on.
 //   fuse         : keyframe X <- (C X + C' T_CkCf Xkf) / (C + C'), C += C'
 #include "m3s_common.hpp"
 #include "m3s_track.h"
@@ -28,6 +27,7 @@ namespace m3s {
 
 #define GN_NSUM 36
 #define GN_PSTRIDE 40
+#define GN_SLOTS 64  // partial-sum slots of the persistent GN launch: one per iteration
 
 // lietorch group product with the product quaternion re-normalised (RxSO3 ctor), float.
 __device__ __forceinline__ void sim3_mul_norm(const float* A, const float* B, float* C) {
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256) track_init_kernel(TrackState* st, const f
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) flags[i] = make_uint4(0u, 0u, 0u, 0u);
   if (i < M3S_TRACK_SHARDS * 16) cnt[i] = 0ull;
-  for (int j = i; j < (M3S_TRACK_SHARDS + 1) * 32; j += gridDim.x * blockDim.x) tick[j] = 0u;
+  for (int j = i; j < M3S_TRACK_TICK_WORDS; j += gridDim.x * blockDim.x) tick[j] = 0u;  // tickets + GnBcast
   if (i != 0) return;
   *st = TrackState{};
   float Ti[8], Tf[8], Tk[8];
@@ -230,10 +230,23 @@ __device__ bool chol7(const double Hd[7][7], const double gd[7], double tau[7]) 
   return true;
 }
 
-// one thread: H, g, cost -> tau -> T update + convergence (tracker.py:156-171, 186-209).
-// T, iter and old_cost come in registers (loaded at kernel start, not re-read on the serial tail).
-__device__ void gn_finish(TrackState* st, const TrackParams& p, const double* sum, const float* T, int iter,
-                          double old, float* T_out, int chunk_id) {
+// one thread: H, g, cost -> tau -> T update + convergence (tracker.py:156-171, 186-209). Pure: the solving
+// block broadcasts the result (GnBcast) and block 0 writes the final state after the loop, so no state
+// byte is written from several XCDs.
+template <typename V>
+__device__ __forceinline__ void wt(V* p, V v) {  // write-through (sc1) store
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct GnStep {
+  float T[8];
+  double cost;
+  int iter, done, status;
+};
+
+__device__ GnStep gn_step(const TrackParams& p, const double* sum, const float* T, int iter, double old) {
+  GnStep r;
+  for (int c = 0; c < 8; c++) r.T[c] = T[c];
   double H[7][7], g[7], tau[7];
   int l = 0;
   for (int c = 0; c < 7; c++)
@@ -243,44 +256,27 @@ __device__ void gn_finish(TrackState* st, const TrackParams& p, const double* su
       l++;
     }
   for (int c = 0; c < 7; c++) g[c] = sum[28 + c];
-  const double cost = sum[35];
-  st->last_cost = cost;
-  if (!chol7(H, g, tau)) {
-    st->status = M3S_TRACK_CHOLESKY_FAILED;
-    st->done = 1;
-    st->done_chunk = chunk_id;
-    return;
-  }
+  r.cost = sum[35];
+  r.iter = iter;
+  r.done = 1;
+  r.status = M3S_TRACK_CHOLESKY_FAILED;
+  if (!chol7(H, g, tau)) return r;
   float tf[7];
   float tn2 = 0.0f;
   for (int c = 0; c < 7; c++) {
     tf[c] = (float)tau[c];
     tn2 += tf[c] * tf[c];
   }
-  float E[8], Tn[8];
+  float E[8];
   expSim3(tf, E);
-  sim3_mul_norm(E, T, Tn);  // T_CkCf.retr(tau) = Exp(tau) * T_CkCf
-  for (int c = 0; c < 8; c++) st->T[c] = Tn[c];
-  const int it = iter + 1;
-  st->iter = it;
+  sim3_mul_norm(E, T, r.T);  // T_CkCf.retr(tau) = Exp(tau) * T_CkCf
+  r.iter = iter + 1;
   // |(old - cost) / old| < rel_error without the divide; inf - x < inf * r is false on the first step,
   // like the reference's inf/inf = nan
-  const bool conv = (fabs(old - cost) < (double)p.rel_error * fabs(old)) || (tn2 < p.delta_norm * p.delta_norm);
-  st->old_cost = cost;
-  if (conv || it >= p.max_iters) {
-    st->status = conv ? M3S_TRACK_OK : M3S_TRACK_MAX_ITERS;
-    st->done = 1;
-    st->done_chunk = chunk_id;
-    float Tk[8], Tw[8];
-    for (int c = 0; c < 8; c++) Tk[c] = st->T_WCk[c];
-    sim3_mul_norm(Tk, Tn, Tw);  // T_WCf = T_WCk * T_CkCf
-    for (int c = 0; c < 8; c++) st->T_WCf[c] = Tw[c];
-    if (T_out != nullptr)
-      for (int c = 0; c < 8; c++) {
-        T_out[c] = Tw[c];
-        T_out[8 + c] = Tn[c];
-      }
-  }
+  const bool conv = (fabs(old - r.cost) < (double)p.rel_error * fabs(old)) || (tn2 < p.delta_norm * p.delta_norm);
+  r.done = conv || r.iter >= p.max_iters;
+  r.status = conv ? M3S_TRACK_OK : (r.done ? M3S_TRACK_MAX_ITERS : M3S_TRACK_RUNNING);
+  return r;
 }
 
 #ifdef M3S_GN_STAMPS  // (experiment builds only) s_memrealtime stamps of block 0 / the last block
@@ -387,11 +383,18 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
   }
 }
 
-__global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackParams p, int chunk_id) {
+// All GN iterations in ONE launch (nparts <= 256 blocks, one per CU, so every block is resident). Per
+// iteration: every block accumulates its points' 36 fp64 sums, publishes them write-through and takes an
+// arrival ticket; the last arriver reduces the partials in a fixed order, solves, retracts, tests
+// convergence and broadcasts {T, cost, iter, done} through the GnBcast record; the other blocks poll
+// its generation word and continue with the new T (no kernel boundary, no empty launches after
+// convergence). Spins are bounded: a stalled hand-off ends the solve (status CHOLESKY_FAILED), never
+// hangs the GPU.
+__global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackParams p) {
   TrackState* st = a.state;
   if (st->done) return;
   const unsigned long long counts = track_counts(a.cnt);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the host readback (same values every launch)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the host readback
     st->n_valid_opt = (int)(unsigned)counts;
     st->n_valid_kf = (int)(unsigned)(counts >> 32);
   }
@@ -402,85 +405,157 @@ __global__ void __launch_bounds__(GN_THREADS) gn_iter_kernel(TrackArgs a, TrackP
     }
     return;
   }
-  const int iter0 = st->iter;
-  const double old_cost = st->old_cost;
-  if (blockIdx.x == 0) GN_STAMP(0);
-  float T[8];
-#pragma unroll
-  for (int c = 0; c < 8; c++) T[c] = st->T[c];
-  double acc[GN_NSUM];
-#pragma unroll
-  for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
-  const float4* rec = reinterpret_cast<const float4*>(a.rec);
-  const int stride = gridDim.x * GN_THREADS;
-  for (int n0 = blockIdx.x * GN_THREADS + threadIdx.x; n0 < p.N; n0 += GN_PPT * stride) {
-    float4 r0[GN_PPT], r1[GN_PPT];
-#pragma unroll
-    for (int u = 0; u < GN_PPT; u++) {
-      const int n = min(n0 + u * stride, p.N - 1);
-      r0[u] = rec[2 * (size_t)n];
-      r1[u] = rec[2 * (size_t)n + 1];
-    }
-#pragma unroll
-    for (int u = 0; u < GN_PPT; u++)
-      if (n0 + u * stride < p.N) gn_point(p, T, r0[u], r1[u], acc);
-  }
-  if (blockIdx.x == 0) GN_STAMP(1);
   __shared__ double s_all[GN_THREADS][GN_LDS_LD];
   __shared__ double s_grp[7][GN_NSUM];
   __shared__ double s_sum[GN_NSUM];
   __shared__ int s_last;
-  block_sum36(acc, s_all, s_grp, s_sum);
-  __syncthreads();
-  if (blockIdx.x == 0) GN_STAMP(2);
-  // publish this block's partial write-through (sc1 agent-scope stores: no release fence needed),
-  // drain, then take a ticket (cdna guide §5 "In-launch split-K reduction")
-  gdouble* part = (gdouble*)a.partials;
-  if (threadIdx.x < GN_NSUM)
-    __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {  // two-level ticket: this block's XCD shard, then the top counter by each shard's last
-    const unsigned sh = blockIdx.x % M3S_TRACK_SHARDS;
-    const unsigned nsh = min(gridDim.x, (unsigned)M3S_TRACK_SHARDS);
-    const unsigned per = (gridDim.x - sh + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;
-    bool last = false;
-    if (__hip_atomic_fetch_add((gu32*)&a.tick[32 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1)
-      last = __hip_atomic_fetch_add((gu32*)&a.tick[32 * M3S_TRACK_SHARDS], 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  GN_STAMP(3);
-  // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r as 16-B vectors in
-  // one round trip, then the same deterministic LDS reduction
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  double v[GN_NSUM];
-  if ((int)threadIdx.x < (int)gridDim.x) {
-    const double2* row = reinterpret_cast<const double2*>(a.partials + (size_t)threadIdx.x * GN_PSTRIDE);
+  __shared__ int s_stop;
+  GnBcast* bc = reinterpret_cast<GnBcast*>(a.tick + 32 * (M3S_TRACK_SHARDS + 1));
+  float T[8];
 #pragma unroll
-    for (int c = 0; c < GN_NSUM / 2; c++) {
-      const double2 t = row[c];
-      v[2 * c] = t.x;
-      v[2 * c + 1] = t.y;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < GN_NSUM; c++) v[c] = 0.0;
-  }
-  block_sum36(v, s_all, s_grp, s_sum);
-  __syncthreads();
-  GN_STAMP(4);
-  if (threadIdx.x == 0) {
-    gn_finish(st, p, s_sum, T, iter0, old_cost, a.T_out, chunk_id);
+  for (int c = 0; c < 8; c++) T[c] = st->T[c];
+  const float4* rec = reinterpret_cast<const float4*>(a.rec);
+  const int stride = gridDim.x * GN_THREADS;
+  for (int it = 0; it < p.max_iters; it++) {
 #ifdef M3S_GN_STAMPS
-    if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
+    const int iter0 = it;
 #endif
+    if (blockIdx.x == 0) GN_STAMP(0);
+    double acc[GN_NSUM];
+#pragma unroll
+    for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
+    for (int n0 = blockIdx.x * GN_THREADS + threadIdx.x; n0 < p.N; n0 += GN_PPT * stride) {
+      float4 r0[GN_PPT], r1[GN_PPT];
+#pragma unroll
+      for (int u = 0; u < GN_PPT; u++) {
+        const int n = min(n0 + u * stride, p.N - 1);
+        r0[u] = rec[2 * (size_t)n];
+        r1[u] = rec[2 * (size_t)n + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < GN_PPT; u++)
+        if (n0 + u * stride < p.N) gn_point(p, T, r0[u], r1[u], acc);
+    }
+    if (blockIdx.x == 0) GN_STAMP(1);
+    block_sum36(acc, s_all, s_grp, s_sum);
+    __syncthreads();
+    if (blockIdx.x == 0) GN_STAMP(2);
+    // publish this block's partial write-through (sc1 agent-scope stores) into the iteration's own slot (a
+    // slot no L2 has seen in this launch), drain, take a ticket
+    const int slot = it < GN_SLOTS ? it : GN_SLOTS - 1;
+    gdouble* part = (gdouble*)(a.partials + (size_t)slot * GN_THREADS * GN_PSTRIDE);
+    if (threadIdx.x < GN_NSUM)
+      __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {  // two-level ticket: this block's XCD shard, then the top counter by each shard's last
+      const unsigned sh = blockIdx.x % M3S_TRACK_SHARDS;
+      const unsigned nsh = min(gridDim.x, (unsigned)M3S_TRACK_SHARDS);
+      const unsigned per = (gridDim.x - sh + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;
+      bool last = false;
+      if (__hip_atomic_fetch_add((gu32*)&a.tick[32 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1)
+        last = __hip_atomic_fetch_add((gu32*)&a.tick[32 * M3S_TRACK_SHARDS], 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+      s_last = last;
+      s_stop = 0;
+    }
+    __syncthreads();
+    if (s_last) {
+      GN_STAMP(3);
+      // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r as 16-B vectors in one
+      // round trip (slots past GN_SLOTS are reused: sc1 loads there), then the deterministic LDS reduction
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      double v[GN_NSUM];
+      if ((int)threadIdx.x < (int)gridDim.x) {
+        if (it < GN_SLOTS - 1) {
+          const double2* row = reinterpret_cast<const double2*>(a.partials + ((size_t)slot * GN_THREADS + threadIdx.x) *
+                                                                                 GN_PSTRIDE);
+#pragma unroll
+          for (int c = 0; c < GN_NSUM / 2; c++) {
+            const double2 t = row[c];
+            v[2 * c] = t.x;
+            v[2 * c + 1] = t.y;
+          }
+        } else {
+          const gdouble* row = part + (size_t)threadIdx.x * GN_PSTRIDE;
+#pragma unroll
+          for (int c = 0; c < GN_NSUM; c++) v[c] = __hip_atomic_load(&row[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < GN_NSUM; c++) v[c] = 0.0;
+      }
+      block_sum36(v, s_all, s_grp, s_sum);
+      __syncthreads();
+      GN_STAMP(4);
+      if (threadIdx.x == 0) {
+        // the previous iteration's cost (the convergence test's old_cost): from the state before the
+        // first solve, from the broadcast record after it
+        const double old = it == 0 ? st->old_cost : __hip_atomic_load(&bc->old_cost, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+        const GnStep r = gn_step(p, s_sum, T, it, old);
+        for (int c = 0; c < 8; c++) __hip_atomic_store(&bc->T[c], r.T[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bc->old_cost, r.cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bc->iter, r.iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bc->status, r.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bc->done, r.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef M3S_GN_STAMPS
+        if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
+      }
+      if (threadIdx.x <= M3S_TRACK_SHARDS)  // every block has arrived: re-arm the tickets for the next iteration
+        __hip_atomic_store((gu32*)&a.tick[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(&bc->gen, (unsigned)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (threadIdx.x == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(&bc->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(it + 1)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 23)) {  // a lost hand-off: stop (status CHOLESKY_FAILED, dx of this frame dropped)
+          s_stop = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_stop) {
+      if (threadIdx.x == 0) {
+        wt(&st->status, M3S_TRACK_CHOLESKY_FAILED);
+        wt(&st->done, 1);
+      }
+      return;
+    }
+    // the new T and the stop flag, sc1 loads after the poll matched (every thread, behind the barrier)
+#pragma unroll
+    for (int c = 0; c < 8; c++) T[c] = __hip_atomic_load(&bc->T[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_load(&bc->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
   }
-  if (threadIdx.x <= M3S_TRACK_SHARDS)  // every block has arrived: re-arm the tickets for the next launch
-    __hip_atomic_store((gu32*)&a.tick[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the final state, written by ONE block (plain stores of a single writer; the host and the fuse launch
+  // read it after this launch)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int status = __hip_atomic_load(&bc->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double cost = __hip_atomic_load(&bc->old_cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->iter = __hip_atomic_load(&bc->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->last_cost = cost;
+    st->old_cost = cost;
+    st->status = status;
+    st->done = 1;
+    st->done_chunk = 0;
+    for (int c = 0; c < 8; c++) st->T[c] = T[c];
+    if (status == M3S_TRACK_OK || status == M3S_TRACK_MAX_ITERS) {
+      float Tk[8], Tw[8];
+      for (int c = 0; c < 8; c++) Tk[c] = st->T_WCk[c];
+      sim3_mul_norm(Tk, T, Tw);  // T_WCf = T_WCk * T_CkCf
+      for (int c = 0; c < 8; c++) st->T_WCf[c] = Tw[c];
+      if (a.T_out != nullptr)
+        for (int c = 0; c < 8; c++) {
+          a.T_out[c] = Tw[c];
+          a.T_out[8 + c] = T[c];
+        }
+    }
+  }
 }
 
 // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf), weighted_pointmap (frame.py:74-77). Runs only if the
@@ -548,11 +623,13 @@ extern "C" hipError_t m3s_launch_track_setup(const TrackArgs* a, const TrackPara
   return hipGetLastError();
 }
 
+// one persistent launch runs every GN iteration (iters and chunk_id are kept for the call sites)
 extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackParams* p, int nparts, int iters,
                                              int chunk_id, hipStream_t s) {
+  (void)iters;
+  (void)chunk_id;
   if (nparts < 1 || nparts > GN_THREADS) return hipErrorInvalidValue;  // the tail loads one partial per thread
-  for (int i = 0; i < iters; i++)
-    hipLaunchKernelGGL(m3s::gn_iter_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p, chunk_id);
+  hipLaunchKernelGGL(m3s::gn_loop_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
   return hipGetLastError();
 }
 

@@ -233,14 +233,24 @@ def retrieval_inputs(seed, C, D, M):
 # ------------------------------------------------------------------------------------------------
 # C4/C5 factor graphs on a recorded trajectory
 # ------------------------------------------------------------------------------------------------
-def chess_poses(K=256):
-    """The first K of 256 7-Scenes chess ground-truth poses (m3s/data/chess_kf256.txt, written by
-    scripts/make_chess_poses.py from groundtruths/7-scenes/chess.txt), (K,8) float64 [t, q xyzw, s]."""
+def _traj(name, K):
     import os
 
-    P = np.loadtxt(os.path.join(os.path.dirname(__file__), "data", "chess_kf256.txt"))
-    assert K <= len(P), f"chess_kf256.txt holds {len(P)} poses"
+    P = np.loadtxt(os.path.join(os.path.dirname(__file__), "data", name))
+    assert K <= len(P), f"{name} holds {len(P)} poses"
     return P[:K]
+
+
+def chess_poses(K=256):
+    """The first K of 256 7-Scenes chess ground-truth poses (m3s/data/chess_kf256.txt, written by
+    scripts/make_traj_poses.py from groundtruths/7-scenes/chess.txt), (K,8) float64 [t, q xyzw, s]."""
+    return _traj("chess_kf256.txt", K)
+
+
+def euroc_poses(K=256):
+    """The first K of 256 EuRoC MH_02_easy ground-truth poses (m3s/data/euroc_mh02_kf256.txt, written by
+    scripts/make_traj_poses.py), (K,8) float64 [t, q xyzw, s]: the C4-shaped (EuRoC) BA graph."""
+    return _traj("euroc_mh02_kf256.txt", K)
 
 
 def _act(T, X):

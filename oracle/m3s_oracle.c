@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <float.h>
+#include <omp.h>
 
 #define M3O_EPS 1e-6 /* gn_kernels.cu:34 */
 
@@ -91,6 +92,9 @@ static inline uint16_t m3o_f2h(float f) {
   if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++;
   return (uint16_t)(sign | q);
 }
+
+/* host threads of the OpenMP loops (bench.py's cpu_baseline times 1 thread and all cores) */
+void m3o_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 void m3o_f32_to_f16(const float* in, uint16_t* out, int64_t n) {
 #pragma omp parallel for schedule(static)

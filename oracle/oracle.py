@@ -73,6 +73,7 @@ def lib():
                                        _i64p, _i64p, _i64p, _u8p, _f32p, _f32p, _f64p, _f64p]
         L.m3o_pose_retr.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int]
         L.m3o_exp_sim3.argtypes = [_f32p, _f32p]
+        L.m3o_set_threads.argtypes = [ctypes.c_int]
         L.m3o_act_sim3.argtypes = [_f32p, _f32p, _f32p]
         L.m3o_rel_sim3.argtypes = [_f32p, _f32p, _f32p]
         _LIB = L
@@ -141,6 +142,11 @@ def ba_params(mode, sigma_a, sigma_b=0.0, C_thresh=0.0, Q_thresh=1.5, K=None, he
         fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
     return np.array([sigma_a, sigma_b, C_thresh, Q_thresh, fx, fy, cx, cy, height, width, pixel_border, z_eps],
                     np.float32)
+
+
+def set_threads(n):
+    """OpenMP threads of the C restatement's parallel loops."""
+    lib().m3o_set_threads(int(n))
 
 
 def gauss_newton(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, params, max_iter, delta_thresh):

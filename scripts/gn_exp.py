@@ -36,4 +36,5 @@ print("iters", tracker.last_result.iters, "(stamps in us from block-0 start; 100
 names = ["b0 start", "b0 loop done", "b0 reduced", "last: ticket", "last: tail loaded", "last: finish done"]
 for it in range(tracker.last_result.iters):
     t0 = buf[it * 16]
-    print(f"iter {it}: " + "  ".join(f"{n}={(buf[it * 16 + k] - t0) / 100:.2f}" for k, n in enumerate(names)))
+    nxt = f"  next b0 start={(buf[(it + 1) * 16] - t0) / 100:.2f}" if it + 1 < tracker.last_result.iters else ""
+    print(f"iter {it}: " + "  ".join(f"{n}={(buf[it * 16 + k] - t0) / 100:.2f}" for k, n in enumerate(names)) + nxt)

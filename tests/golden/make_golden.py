@@ -7,7 +7,8 @@ travels: only the resulting .npz vectors are committed. What runs from the refer
   mast3r_slam/image.py        img_gradient
   mast3r_slam/geometry.py     point_to_ray_dist, act_Sim3, project_calib, constrain_points_to_ray, ...
   mast3r_slam/tracker.py      FrameTracker.track / opt_pose_ray_dist_sim3 / opt_pose_calib_sim3 / solve
-  mast3r_slam/global_opt.py   FactorGraph.solve_GN_rays / solve_GN_calib (prep_two_way_edges, pin, write-back)
+  mast3r_slam/global_opt.py   FactorGraph.solve_GN_rays / solve_GN_calib (prep_two_way_edges, pin, write-back),
+                              FactorGraph.add_factors (Q filter, min-match fraction, consecutive rule, reloc)
   mast3r_slam/frame.py        Frame.update_pointmap (weighted_pointmap fusion)
   mast3r_slam/retrieval_database.py  RetrievalDatabase.quantize_custom (distance GEMM + top-k), called
                               unbound on a stand-in `self` holding the centroids
@@ -257,6 +258,77 @@ def gen_ba(n_kf=6, H=24, W=32, seed=1):
          rays_Twc=res["rays"], calib_Twc=res["calib"])
 
 
+# ---------------------------------------------------------------- FactorGraph.add_factors
+def _sym_outputs(seed, H, W, kind):  # restated in tests/test_gpu_factor_graph.py (the inputs are regenerated)
+    """Synthetic symmetric-decoder outputs of one keyframe pair, ordered (ii, ji, jj, ij) like
+    mast3r_decode_symmetric_batch: the i->j pair from one synthetic pair, the j->i pair from another.
+    kind 'good': natural confidences; 'poor': every Q = 1 (no match passes Q_conf); 'one_sided': Qjj = Qij
+    = 1 (the j->i direction fails, i->j passes)."""
+    A = synthetic.make_pair(H, W, seed=seed)
+    B = synthetic.make_pair(H, W, seed=seed + 1000)
+    X = torch.stack((A["X"][0], A["X"][1], B["X"][0], B["X"][1]))
+    C = torch.stack((A["C"][0], A["C"][1], B["C"][0], B["C"][1]))
+    D = torch.stack((A["D"][0], A["D"][1], B["D"][0], B["D"][1]))
+    Q = torch.stack((A["Q"][0], A["Q"][1], B["Q"][0], B["Q"][1]))
+    if kind == "poor":
+        Q = torch.ones_like(Q)
+    elif kind == "one_sided":
+        Q[2:] = 1.0
+    return X, C, D, Q
+
+
+def gen_add_factors(H=32, W=48):
+    """The reference's FactorGraph.add_factors (global_opt.py:32-101) over four calls on synthetic symmetric
+    decoder outputs, the matcher being the reference's matching.match over the C oracle. Covers the Q filter,
+    the both-directions min-match-fraction rule, the consecutive-edge exemption, the is_reloc early return
+    (state untouched) and the append order."""
+    calls = [  # (ii, jj, kinds, min_match_frac, is_reloc)
+        ([0, 1, 0], [1, 2, 2], ["good", "poor", "one_sided"], ref_config.config["local_opt"]["min_match_frac"], False),
+        ([2, 0], [3, 3], ["good", "good"], ref_config.config["local_opt"]["min_match_frac"], False),
+        ([1, 2], [4, 4], ["poor", "good"], ref_config.config["reloc"]["min_match_frac"], True),
+        ([3], [4], ["poor"], ref_config.config["reloc"]["min_match_frac"], True),
+    ]
+    queue = []
+
+    def match_symmetric(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+        # mast3r_utils.py:149-187 on the queued decoder outputs
+        X, C, D, Q = queue.pop(0)
+        b = X.shape[1]
+        X11 = torch.cat((X[0], X[2]), dim=0)
+        X21 = torch.cat((X[1], X[3]), dim=0)
+        D11 = torch.cat((D[0], D[2]), dim=0)
+        D21 = torch.cat((D[1], D[3]), dim=0)
+        idx_1_to_2, valid_match_2 = ref_matching.match(X11, X21, D11, D21)
+        return (idx_1_to_2[:b], idx_1_to_2[b:], valid_match_2[:b], valid_match_2[b:], Q[0].view(b, -1, 1),
+                Q[2].view(b, -1, 1), Q[1].view(b, -1, 1), Q[3].view(b, -1, 1))
+
+    ref_go.mast3r_match_symmetric = match_symmetric
+
+    class _KF:
+        feat = torch.zeros(1, 1)
+        pos = torch.zeros(1, 1, 2)
+        img_true_shape = torch.tensor([[H, W]])
+
+    fg = ref_go.FactorGraph(None, [_KF() for _ in range(5)], device="cpu")
+    out = {}
+    for c, (ii, jj, kinds, mmf, reloc) in enumerate(calls):
+        outs = [_sym_outputs(100 * c + 10 * e, H, W, k) for e, k in enumerate(kinds)]
+        X, C, D, Q = (torch.stack([o[t] for o in outs], dim=1) for t in range(4))  # (4, b, H, W, ...)
+        queue.append((X, C, D, Q))
+        ret = fg.add_factors(ii, jj, mmf, is_reloc=reloc)
+        # the inputs are regenerated by the test from (seed, kind) with m3s.synthetic; a checksum pins them
+        csum = np.array([float(t.double().sum()) for t in (X, C, D, Q)])
+        out.update({f"c{c}_seeds": np.array([100 * c + 10 * e for e in range(len(kinds))]),
+                    f"c{c}_kinds": np.array(kinds), f"c{c}_csum": csum, f"c{c}_ii": np.array(ii), f"c{c}_jj": np.array(jj), f"c{c}_mmf": np.float32(mmf),
+                    f"c{c}_reloc": np.bool_(reloc), f"c{c}_ret": np.bool_(bool(ret)),
+                    f"c{c}_ii_out": _np(fg.ii), f"c{c}_jj_out": _np(fg.jj), f"c{c}_idx_ii2jj": _np(fg.idx_ii2jj),
+                    f"c{c}_idx_jj2ii": _np(fg.idx_jj2ii), f"c{c}_valid_j": _np(fg.valid_match_j),
+                    f"c{c}_valid_i": _np(fg.valid_match_i), f"c{c}_Q_ii2jj": _np(fg.Q_ii2jj),
+                    f"c{c}_Q_jj2ii": _np(fg.Q_jj2ii)})
+    out["ncalls"] = np.int32(len(calls))
+    save(f"add_factors_{H}x{W}.npz", **out)
+
+
 # ---------------------------------------------------------------- oracle BA rows vs reference geometry
 def gen_ba_rows(N=512, seed=11):
     """With T_i = identity the adjoint is I, so the oracle's H_jj / g_j for one edge must equal the
@@ -345,3 +417,4 @@ if __name__ == "__main__":
     gen_ba()
     gen_ba_rows()
     gen_retrieval()
+    gen_add_factors()
