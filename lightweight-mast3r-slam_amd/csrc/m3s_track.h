@@ -60,17 +60,18 @@ struct TrackArgs {
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
 };
 
-// Per-iteration broadcast of the persistent GN launch: written write-through (sc1) by the block that
-// solved iteration `gen`-1, read with sc1 loads by every block once it sees `gen` (MI355X_MICROARCH.md
-// "Hand-offs measured with sc1 loads": one storing lane, sc1 flag, sc1 loads after the poll matched).
+// Per-iteration broadcast of the persistent GN launch, written write-through (sc1) by the block that
+// solved the iteration: 8-byte {data, tag} granules (MI355X_MICROARCH.md, persistent-kernel price list,
+// "Granule"), polled with sc1 loads; old_cost / iter / status are stored before the granules (drained)
+// and read only by the next solving block.
 struct GnBcast {
-  float T[8];       // T_CkCf after the last solved iteration
+  // granules {value bits, generation}: T_CkCf[0..7] and the done flag of the last solved iteration; a
+  // block polls them directly (the tag says the value is the new one: no separate flag round trip)
+  unsigned long long g[9];
   double old_cost;  // that iteration's cost (the next convergence test's old_cost)
   int iter;         // iterations done
-  int done;         // converged / max iterations / Cholesky failure
   int status;       // M3S_TRACK_*
-  unsigned gen;     // iterations published
-  int pad[2];
+  int pad[4];
 };
 #define M3S_TRACK_TICK_WORDS ((M3S_TRACK_SHARDS + 1 + 2) * 32)
 

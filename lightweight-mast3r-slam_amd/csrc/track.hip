@@ -410,6 +410,8 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   __shared__ double s_sum[GN_NSUM];
   __shared__ int s_last;
   __shared__ int s_stop;
+  __shared__ float s_T[8];
+  __shared__ int s_bc[9];
   GnBcast* bc = reinterpret_cast<GnBcast*>(a.tick + 32 * (M3S_TRACK_SHARDS + 1));
   float T[8];
 #pragma unroll
@@ -463,8 +465,9 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     __syncthreads();
     if (s_last) {
       GN_STAMP(3);
-      // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r as 16-B vectors in one
-      // round trip (slots past GN_SLOTS are reused: sc1 loads there), then the deterministic LDS reduction
+      // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r of this iteration's
+      // slot (no L2 has held it in this launch) as 16-B vectors in one round trip, then the deterministic LDS
+      // reduction; past GN_SLOTS - 1 iterations the last slot is reused and read with sc1 loads
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       double v[GN_NSUM];
       if ((int)threadIdx.x < (int)gridDim.x) {
@@ -495,11 +498,11 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
         const double old = it == 0 ? st->old_cost : __hip_atomic_load(&bc->old_cost, __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_AGENT);
         const GnStep r = gn_step(p, s_sum, T, it, old);
-        for (int c = 0; c < 8; c++) __hip_atomic_store(&bc->T[c], r.T[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&bc->old_cost, r.cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&bc->iter, r.iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&bc->status, r.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&bc->done, r.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_bc[8] = r.done;
+        for (int c = 0; c < 8; c++) s_T[c] = r.T[c];
 #ifdef M3S_GN_STAMPS
         if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -508,16 +511,30 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
         __hip_atomic_store((gu32*)&a.tick[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(&bc->gen, (unsigned)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (threadIdx.x == 0) {
+      if (threadIdx.x < 9) {  // the granules, after everything above has drained
+        const unsigned val = threadIdx.x < 8 ? __float_as_uint(s_T[threadIdx.x]) : (unsigned)s_bc[8];
+        __hip_atomic_store(&bc->g[threadIdx.x], ((unsigned long long)(it + 1) << 32) | val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (threadIdx.x < 64) {
+      // wave 0 polls the 9 granules (one lane each) until every tag is this iteration's
       unsigned spins = 0;
-      while (__hip_atomic_load(&bc->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(it + 1)) {
-        __builtin_amdgcn_s_sleep(2);
+      unsigned long long gv = 0;
+      for (;;) {
+        bool ok = true;
+        if (threadIdx.x < 9) {
+          gv = __hip_atomic_load(&bc->g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = (unsigned)(gv >> 32) == (unsigned)(it + 1);
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 23)) {  // a lost hand-off: stop (status CHOLESKY_FAILED, dx of this frame dropped)
-          s_stop = 1;
+          if (threadIdx.x == 0) s_stop = 1;
           break;
         }
       }
+      if (threadIdx.x < 8) s_T[threadIdx.x] = __uint_as_float((unsigned)gv);
+      if (threadIdx.x == 8) s_bc[8] = (int)(unsigned)gv;
     }
     __syncthreads();
     if (s_stop) {
@@ -527,10 +544,11 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       }
       return;
     }
-    // the new T and the stop flag, sc1 loads after the poll matched (every thread, behind the barrier)
 #pragma unroll
-    for (int c = 0; c < 8; c++) T[c] = __hip_atomic_load(&bc->T[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_load(&bc->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    for (int c = 0; c < 8; c++) T[c] = s_T[c];
+    const bool fin = s_bc[8] != 0;
+    __syncthreads();  // s_T / s_bc are rewritten in the next iteration
+    if (fin) break;
   }
   // the final state, written by ONE block (plain stores of a single writer; the host and the fuse launch
   // read it after this launch)
