@@ -432,10 +432,12 @@ struct BaPlanImpl {
 };
 static_assert(sizeof(BaPlanImpl) <= sizeof(m3s_ba_plan), "m3s_ba_plan too small");
 
+// points of one keyframe per linearisation block: 24576 x 12 B = 295 KB of X_j, so the ~100 blocks an XCD
+// runs at once (the edges of a few target keyframes, same chunk) share their X_j slabs in its 4 MiB L2
+constexpr int BA_CHUNK_POINTS = 24576;
 int ba_chunks(int N, int E) {
-  const int want = (2048 + std::max(E, 1) - 1) / std::max(E, 1);
-  const int cap = std::max(1, (N + 4095) / 4096);
-  return std::max(1, std::min(want, cap));
+  (void)E;
+  return std::max(1, (N + BA_CHUNK_POINTS - 1) / BA_CHUNK_POINTS);
 }
 
 constexpr int BA_DENSE_MAX_POSES = 1025;  // dense fallback workspace: (2n+1) n doubles, ~0.8 GB at this size
@@ -448,18 +450,19 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_BLOB_SECTIONS = 19;
+constexpr int BA_BLOB_SECTIONS = 20;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
 inline size_t ba_max_pairs(int Kp) {
   const size_t nb = (size_t)std::max(0, Kp - 1);
   return std::min(nb * nb * nb / 6 + nb * nb + 64, 32 * ba_max_blocks(Kp) + 64);
 }
-size_t ba_blob_capacity(int Kp, int E) {
+size_t ba_blob_capacity(int Kp, int E, int chunks) {
   const size_t nb = (size_t)std::max(0, Kp - 1), nLm = ba_max_blocks(Kp);
   // ranks, perm, col_ptr, rowL, lev_ptr, lev_col, grp_ptr, grp, pull_grp, src, sidx, asm CSR, rhs CSR
   const size_t ints = 2 * (size_t)E + nb + (nb + 1) + nLm + (nb + 1) + nb + (nb + 2) + 4 * nLm + nb + 4 * nLm +
-                      ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E;
+                      ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E +
+                      (size_t)E * chunks;  // + the linearisation block table
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -479,7 +482,7 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   a->info = c.take<int>(4);
   a->done = a->info + 1;
   a->iters = a->info + 2;
-  *blob = c.take<char>(ba_blob_capacity(Kp, E));
+  *blob = c.take<char>(ba_blob_capacity(Kp, E, chunks));
   return c.off;
 }
 
@@ -571,6 +574,22 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   // symbolic factorisation of the pose system (SparseBlock's pattern, gn_kernels.cu:71-113)
   BaPattern S;
   ba_build_pattern(ri.data(), rj.data(), E, Kp, &S);
+  // linearisation block table: this shard's edges grouped by target keyframe j, chunk-major within a
+  // group, so consecutive blocks (dealt to one XCD by xcd_remap) read the same X_j slab
+  std::vector<int> lin_tab;
+  {
+    std::vector<int> order(e1 - e0);
+    for (int e = 0; e < e1 - e0; e++) order[e] = e;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return rj[e0 + x] < rj[e0 + y]; });
+    lin_tab.reserve((size_t)(e1 - e0) * chunks);
+    for (size_t g0 = 0; g0 < order.size();) {
+      size_t g1 = g0;
+      while (g1 < order.size() && rj[e0 + order[g1]] == rj[e0 + order[g0]]) g1++;
+      for (int c = 0; c < chunks; c++)
+        for (size_t t = g0; t < g1; t++) lin_tab.push_back(order[t] * chunks + c);
+      g0 = g1;
+    }
+  }
   // pack every table into one staging image of the device blob
   struct Sec {
     const void* src;
@@ -597,11 +616,12 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       {S.asm_ent.data(), sizeof(int) * S.asm_ent.size(), (const void**)&P.a.asm_ent},
       {S.rhs_ptr.data(), sizeof(int) * S.rhs_ptr.size(), (const void**)&P.a.rhs_ptr},
       {S.rhs_ent.data(), sizeof(int) * S.rhs_ent.size(), (const void**)&P.a.rhs_ent},
+      {lin_tab.data(), sizeof(int) * lin_tab.size(), (const void**)&P.a.lin_tab},
   };
   static_assert(sizeof(secs) / sizeof(secs[0]) == BA_BLOB_SECTIONS, "blob sections");
   size_t total = 0;
   for (const Sec& x : secs) total += (x.bytes + 15) & ~(size_t)15;
-  if (S.sidx.size() > ba_max_pairs(Kp) || total > ba_blob_capacity(Kp, E))
+  if (S.sidx.size() > ba_max_pairs(Kp) || total > ba_blob_capacity(Kp, E, chunks))
     return fail(M3S_EINVAL, "ba: factor pattern too dense for the plan tables");
   {
     PlanStage& st = plan_stage();

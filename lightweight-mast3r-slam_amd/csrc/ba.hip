@@ -35,9 +35,12 @@ namespace m3s {
 // MASK: the row's structurally nonzero Jacobian entries (bit c). Products with a structural zero
 // are skipped: for finite weights they add an exact +-0 to the sum, so the result is unchanged
 // (the reference computes them; ~45% of the FMAs in rays mode).
-// Products and sums in fp64 from the fp32 rows: fp64 FMA issues at the fp32 (unpacked) rate on
-// CDNA, and it keeps the whole BA within 1e-5 of the fp64 truth (fp32 products put the
-// ill-conditioned 6-KF golden at ~1.2e-5).
+// BA_RUN_LEN > 0: products and sums in fp32 over runs of BA_RUN_LEN points per lane, each run added to the
+// fp64 accumulators (packed fp32 FMAs instead of fp64 ones: the kernel is VALU-issue bound); 0: products
+// and sums in fp64 from the fp32 rows.
+#ifndef BA_RUN_LEN
+#define BA_RUN_LEN 4
+#endif
 template <unsigned MASK>
 __device__ __forceinline__ void acc_local(double* L, double* v, const float J[7], float w, float e) {
   double Jd[7];
@@ -56,6 +59,33 @@ __device__ __forceinline__ void acc_local(double* L, double* v, const float J[7]
     if ((MASK >> c) & 1u) v[c] += wj * ed;
   }
 }
+
+template <unsigned MASK>
+__device__ __forceinline__ void acc_local_f32(float* L, float* v, const float J[7], float w, float e) {
+  int l = 0;
+#pragma unroll
+  for (int c = 0; c < 7; c++) {
+    const float wj = w * J[c];
+#pragma unroll
+    for (int d = c; d < 7; d++) {
+      if ((MASK >> c) & (MASK >> d) & 1u) L[l] = fmaf(wj, J[d], L[l]);
+      l++;
+    }
+    if ((MASK >> c) & 1u) v[c] = fmaf(wj, e, v[c]);
+  }
+}
+
+#ifndef BA_PPT  // points per lane per round of the linearisation loop (loads first)
+#define BA_PPT 2
+#endif
+#ifndef BA_LIN_WAVES  // waves per SIMD the linearisation is compiled for (VGPR budget 512 / waves)
+#define BA_LIN_WAVES (BA_RUN_LEN > 0 ? 3 : 4)
+#endif
+#if BA_RUN_LEN > 0
+#define ACC_ROW(MASK, J, W, E) acc_local_f32<MASK>(fL, fv, J, W, E)
+#else
+#define ACC_ROW(MASK, J, W, E) acc_local<MASK>(L, v, J, W, E)
+#endif
 
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
 //   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
@@ -91,10 +121,12 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
 }
 
 template <int MODE>  // specialised per residual type: one mode's registers, not the union of three
-__global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
+__global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaParams p) {
   if (*a.done) return;
-  const int e = blockIdx.x / p.chunks;
-  const int chunk = blockIdx.x % p.chunks;
+  // the plan's block table: edges grouped by target keyframe, consecutive blocks on one XCD (xcd_remap)
+  const int code = a.lin_tab[xcd_remap(blockIdx.x, gridDim.x)];
+  const int e = code / p.chunks;
+  const int chunk = code - e * p.chunks;
   const int N = p.N;
   const int ix = a.ii_rank[e], jx = a.jj_rank[e];
   float Ti[8], Tj[8], Tij[8];
@@ -114,9 +146,30 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
   const int k_end = min(N, k_begin + per);
-  for (int k = k_begin + threadIdx.x; k < k_end; k += blockDim.x) {
-    const float4 R = rec[k];
-    const float Xj[3] = {Xj_base[(size_t)k * 3], Xj_base[(size_t)k * 3 + 1], Xj_base[(size_t)k * 3 + 2]};
+#if BA_RUN_LEN > 0
+  float fL[28], fv[7];
+#pragma unroll
+  for (int c = 0; c < 28; c++) fL[c] = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 7; c++) fv[c] = 0.0f;
+  int run = 0;
+#endif
+  // BA_PPT points per lane per round: every round's record / Xj loads are issued before its math
+  for (int k0 = k_begin + threadIdx.x; k0 < k_end; k0 += BA_PPT * blockDim.x) {
+    float4 Rr[BA_PPT];
+    float Xjr[BA_PPT][3];
+#pragma unroll
+    for (int u = 0; u < BA_PPT; u++) {
+      const int k = min(k0 + u * (int)blockDim.x, k_end - 1);
+      Rr[u] = rec[k];
+#pragma unroll
+      for (int c = 0; c < 3; c++) Xjr[u][c] = Xj_base[(size_t)k * 3 + c];
+    }
+#pragma unroll
+    for (int u = 0; u < BA_PPT; u++) {
+    if (k0 + u * (int)blockDim.x >= k_end) break;
+    const float4 R = Rr[u];
+    const float Xj[3] = {Xjr[u][0], Xjr[u][1], Xjr[u][2]};
     float Y[3];
     actSO3(&Tij[3], Xj, Y);  // actSim3 (gn_kernels.cu:207-219): rotate, scale, translate
     Y[0] = Y[0] * Tij[7];
@@ -134,9 +187,9 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       const float J0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
       const float J1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
       const float J2[7] = {0.0f, 0.0f, 1.0f, Y[1], -Y[0], 0.0f, Y[2]};
-      acc_local<0b1110001>(L, v, J0, huber_ba(sw * err[0]) * wc, err[0]);  // {0,4,5,6}
-      acc_local<0b1101010>(L, v, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
-      acc_local<0b1011100>(L, v, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
+      ACC_ROW(0b1110001, J0, huber_ba(sw * err[0]) * wc, err[0]);  // {0,4,5,6}
+      ACC_ROW(0b1101010, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
+      ACC_ROW(0b1011100, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
     } else if constexpr (MODE == BA_MODE_RAYS) {
       const float Xi[3] = {R.x, R.y, R.z};
       const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
@@ -161,10 +214,10 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.0f, rj[0], 0.0f};
       const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.0f, 0.0f};
       const float J3[7] = {rj[0], rj[1], rj[2], 0.0f, 0.0f, 0.0f, n1j};
-      acc_local<0b0110111>(L, v, J0, huber_ba(swr * err[0]) * wr, err[0]);  // {0,1,2,4,5}
-      acc_local<0b0101111>(L, v, J1, huber_ba(swr * err[1]) * wr, err[1]);  // {0,1,2,3,5}
-      acc_local<0b0011111>(L, v, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
-      acc_local<0b1000111>(L, v, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
+      ACC_ROW(0b0110111, J0, huber_ba(swr * err[0]) * wr, err[0]);  // {0,1,2,4,5}
+      ACC_ROW(0b0101111, J1, huber_ba(swr * err[1]) * wr, err[1]);  // {0,1,2,3,5}
+      ACC_ROW(0b0011111, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
+      ACC_ROW(0b1000111, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
       const float u_t = R.x, v_t = R.y, zi = R.z;
       const bool valid_z = (Y[2] > p.z_eps) && (zi > p.z_eps);
@@ -184,11 +237,33 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
       const float J0[7] = {fx * zj_inv, 0.0f, -fx * xz * zj_inv, -fx * xz * yz, fx * (1 + xz * xz), -fx * yz, 0.0f};
       const float J1[7] = {0.0f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1 + yz * yz), fy * xz * yz, fy * xz, 0.0f};
       const float J2[7] = {0.0f, 0.0f, zj_inv, yz, -xz, 0.0f, 1.0f};
-      acc_local<0b0111101>(L, v, J0, huber_ba(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
-      acc_local<0b0111110>(L, v, J1, huber_ba(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
-      acc_local<0b1011100>(L, v, J2, huber_ba(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
+      ACC_ROW(0b0111101, J0, huber_ba(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
+      ACC_ROW(0b0111110, J1, huber_ba(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
+      ACC_ROW(0b1011100, J2, huber_ba(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
+    }  // u
+#if BA_RUN_LEN > 0
+    if (++run == BA_RUN_LEN) {  // the run's fp32 sums into the fp64 accumulators
+      run = 0;
+#pragma unroll
+      for (int c = 0; c < 28; c++) {
+        L[c] += (double)fL[c];
+        fL[c] = 0.0f;
+      }
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        v[c] += (double)fv[c];
+        fv[c] = 0.0f;
+      }
+    }
+#endif
   }
+#if BA_RUN_LEN > 0
+#pragma unroll
+  for (int c = 0; c < 28; c++) L[c] += (double)fL[c];
+#pragma unroll
+  for (int c = 0; c < 7; c++) v[c] += (double)fv[c];
+#endif
   // wave64 butterfly in fp64, then 4 waves through LDS
   __shared__ double s_part[4][BA_NSUM];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -205,7 +280,7 @@ __global__ void __launch_bounds__(256, 4) ba_lin_kernel(BaArgs a, BaParams p) {
   __syncthreads();
   if (threadIdx.x < 35) {
     const int c = threadIdx.x;
-    a.partials[(size_t)blockIdx.x * BA_NSUM + c] = s_part[0][c] + s_part[1][c] + s_part[2][c] + s_part[3][c];
+    a.partials[(size_t)code * BA_NSUM + c] = s_part[0][c] + s_part[1][c] + s_part[2][c] + s_part[3][c];
   }
 }
 

@@ -51,6 +51,7 @@ struct BaArgs {
   const int* asm_ent;
   const int* rhs_ptr;     // (nb+1) per factor row
   const int* rhs_ent;
+  const int* lin_tab;     // (E_local * chunks) linearisation block -> local edge * chunks + chunk
   double* L;   // (nL, 8, 8) factor blocks (7x7 used; diagonal blocks keep 1/L_mm in column 7)
   double* y;   // (nb, 8) rhs -> forward-substituted
   double* xs;  // (nb, 8) solution in factor order

@@ -1,5 +1,5 @@
 """BA experiment: per-iteration linearize / solve time (HIP-event spans in libm3s) on a synthetic graph.
-usage: python scripts/ba_exp.py [K] [H] [W] [iters] [graph: circle|chess] [mode: rays|calib]"""
+usage: python scripts/ba_exp.py [K] [H] [W] [iters] [graph: circle|chess|euroc] [mode: rays|calib]"""
 import ctypes
 import os
 import sys
@@ -13,7 +13,7 @@ import torch  # noqa: E402
 from m3s import _lib  # noqa: E402
 from m3s.config import config  # noqa: E402
 from m3s.dist_ba import HipShard, ba_config, run_sharded  # noqa: E402
-from m3s.synthetic import chess_poses, make_graph, make_traj_graph  # noqa: E402
+from m3s.synthetic import chess_poses, euroc_poses, make_graph, make_traj_graph  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 384
@@ -23,8 +23,8 @@ graph = sys.argv[5] if len(sys.argv) > 5 else "circle"
 mode = sys.argv[6] if len(sys.argv) > 6 else "rays"
 dev = torch.device("cuda")
 t0 = time.time()
-if graph == "chess":  # the 7-Scenes chess trajectory, built on the GPU
-    G = make_traj_graph(chess_poses(K), H, W, seed=1, device=dev)
+if graph in ("chess", "euroc"):  # SURVEY §8(d) C5 / C4 trajectories, built on the GPU
+    G = make_traj_graph((chess_poses if graph == "chess" else euroc_poses)(K), H, W, seed=1, device=dev)
     ii, jj, idx = G["ii"], G["jj"], G["idx"].contiguous()
     valid, Q = G["valid"][..., 0].contiguous(), G["Q"][..., 0].contiguous()
 else:
