@@ -31,7 +31,7 @@ hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*
                                  void*, int*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
-hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, hipStream_t);
+hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, const TrackPublish*, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
@@ -268,18 +268,34 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
 // ------------------------------------------------------------------------------------------
 // GN blocks: 2 points per lane at 512x512 (512 blocks = 2 per CU), at most 512 partials to reduce
 // pinned host copy of the device state: the one per-frame readback is a direct DMA, not a staged copy
-static TrackState* pinned_state() {
-  static thread_local TrackState* h = nullptr;
+// Per host thread: the frame result mirror in fine-grained pinned memory (the fuse launch writes it).
+static TrackMirror* pinned_mirror() {
+  static thread_local TrackMirror* h = nullptr;
   if (h == nullptr) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, sizeof(TrackState), hipHostMallocDefault) != hipSuccess) {
-      static thread_local TrackState fallback;  // pageable: still correct, slower copy
-      h = &fallback;
-    } else {
-      h = static_cast<TrackState*>(p);
-    }
+    if (hipHostMalloc(&p, sizeof(TrackMirror), hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+      return nullptr;
+    h = static_cast<TrackMirror*>(p);
+    memset(h, 0, sizeof(TrackMirror));
   }
   return h;
+}
+
+// Wait for generation `gen` in the mirror: a spin on the host-coherent word (no interrupt wake-up, no
+// D2H copy kernel), with a stream query every 1024 polls so a failed or drained stream ends the wait.
+static int wait_published(const TrackMirror* m, unsigned gen, hipStream_t s) {
+  for (unsigned spin = 1;; spin++) {
+    if (__atomic_load_n(&m->gen, __ATOMIC_ACQUIRE) == gen) return M3S_OK;
+    if ((spin & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&m->gen, __ATOMIC_ACQUIRE) == gen) return M3S_OK;
+        return fail(M3S_EHIP, "track: stream drained without publishing the frame state");
+      }
+      if (q != hipErrorNotReady) return fail(M3S_EHIP, std::string("track sync: ") + hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
@@ -393,16 +409,21 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   }
   (void)first_chunk;  // every GN iteration runs inside one persistent launch (gn_loop_kernel)
   const int nparts = track_nparts(N);
-  TrackState& hs = *pinned_state();
+  TrackMirror* mirror = pinned_mirror();
+  if (mirror == nullptr) return fail(M3S_EHIP, "track: pinned result mirror allocation failed");
+  static thread_local unsigned gen = 0;
+  TrackPublish pub{mirror, a.tick + M3S_TRACK_PUBLISH_TICKET, ++gen};
   {
     Span sp("gn_iters", s);
     HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, p.max_iters, 0, s), "track iterate launch");
   }
   // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
   // before the readback, it runs only if the solve finished with a pose
-  if (do_fuse || !p.direct) HIP_TRY(m3s_launch_fuse(&a, 0, &fa, p.direct ? 0 : 1, N, s), "track fuse launch");
-  HIP_TRY(hipMemcpyAsync(&hs, st, sizeof(TrackState), hipMemcpyDeviceToHost, s), "track readback");
-  HIP_TRY(hipStreamSynchronize(s), "track sync");
+  // The same launch publishes the result to the host mirror; the call returns once it has (the fusion
+  // blocks may still be running: later work on this stream is ordered after them).
+  HIP_TRY(m3s_launch_fuse(&a, 0, &fa, p.direct ? 0 : 1, N, &pub, s), "track fuse launch");
+  if (int rc = wait_published(mirror, pub.gen, s)) return rc;
+  const TrackState& hs = mirror->s;
   memcpy(result->T_WCf, hs.T_WCf, sizeof(result->T_WCf));
   memcpy(result->T_CkCf, hs.T, sizeof(result->T_CkCf));
   result->cost = hs.last_cost;

@@ -73,7 +73,23 @@ struct GnBcast {
   int status;       // M3S_TRACK_*
   int pad[4];
 };
-#define M3S_TRACK_TICK_WORDS ((M3S_TRACK_SHARDS + 1 + 2) * 32)
+// tickets (8 shards + top), the GnBcast record (two lines), the fuse kernel's publish ticket (one line)
+#define M3S_TRACK_TICK_WORDS ((M3S_TRACK_SHARDS + 1 + 2 + 1) * 32)
+#define M3S_TRACK_PUBLISH_TICKET ((M3S_TRACK_SHARDS + 1 + 2) * 32)
+
+// The frame's result as the host reads it: a copy of the final TrackState in fine-grained (coherent)
+// pinned host memory, written by the fuse launch once n_unique is complete and then released with the
+// call's generation number; the host spins on gen instead of a D2H copy + hipStreamSynchronize.
+struct TrackMirror {
+  TrackState s;
+  unsigned gen;
+  unsigned pad[3];
+};
+struct TrackPublish {
+  TrackMirror* mirror;  // host pointer (the same address on the device for hipHostMalloc memory)
+  unsigned* ticket;     // tick + M3S_TRACK_PUBLISH_TICKET (zeroed by track_init)
+  unsigned gen;
+};
 
 // keyframe fusion (weighted_pointmap) + the match_info average confidences (frame.py:74-77, 83-84)
 struct FuseArgs {

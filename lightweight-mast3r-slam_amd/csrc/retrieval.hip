@@ -213,6 +213,9 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
     }
     asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");  // this wave's k-step s+1 query copies landed ...
     __builtin_amdgcn_s_barrier();                      // ... and every wave's; image `buf` no longer read
+    // the ring registers are defined by the asm loads, so the compiler sees no dependence on the wait above:
+    // a scheduling fence keeps the next step's MFMAs (pure register ops) from being hoisted across it
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
   };
   const std::integral_constant<int, 0> I0;
@@ -222,6 +225,7 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
   aload(A1, min(1, S - 1));
   stage_b(0, sb0_);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
   for (int s = 0; s < S; s += 6) {  // 6 = lcm(3 register slots, 2 LDS images): every selection compile-time
     step(I0, s, A0, A2);
@@ -232,6 +236,7 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
     if (s + 5 < S) step(I1, s + 5, A2, A1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-loads
+  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
 
   // ---- epilogue: exact block top-K per query by a threshold filter ----

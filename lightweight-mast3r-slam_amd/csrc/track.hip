@@ -581,31 +581,48 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
 // back). Out of place like the reference (new X_canon / C tensors); X_out may alias X_in.
 #define FUSE_COUNT_BLOCKS 32
 
+// Thread 0 of each counting block arrives after its own n_unique add (the acq_rel ticket orders it); the
+// last of the FUSE_COUNT_BLOCKS blocks to arrive copies the final state (n_unique now
+// complete) to the host mirror and releases the call's generation at system scope.
+__device__ void publish_state(const TrackState* st, TrackPublish pub) {
+  if (__hip_atomic_fetch_add(pub.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != FUSE_COUNT_BLOCKS - 1)
+    return;
+  TrackState v = *st;
+  v.n_unique = __hip_atomic_load(&const_cast<TrackState*>(st)->n_unique, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  pub.mirror->s = v;
+  __hip_atomic_store(&pub.mirror->gen, pub.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id, FuseArgs f,
-                                                   int N, const uint8_t* __restrict__ flags, int* __restrict__ n_unique) {
-  if (!(st->done && st->done_chunk == chunk_id)) return;
+                                                   int N, const uint8_t* __restrict__ flags, int* __restrict__ n_unique,
+                                                   TrackPublish pub) {
+  const bool solved = st->done && st->done_chunk == chunk_id;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n_unique != nullptr && blockIdx.x < FUSE_COUNT_BLOCKS) {
-    // |unique(idx[valid])| (tracker.py:106-108): popcount of the byte map track_setup wrote (0/1 bytes,
-    // 16-B padded), here after the solve instead of on the first GN iteration's critical path. A few
-    // blocks reduce in LDS and add once each: one device-scope atomic per block, not per wave.
-    __shared__ int s_cnt[4];
-    const uint4* fl = reinterpret_cast<const uint4*>(flags);
-    const int n16 = (N + 15) / 16;
-    int cnt = 0;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += FUSE_COUNT_BLOCKS * 256) {
-      const uint4 v = fl[i];
-      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-    }
+  if (blockIdx.x < FUSE_COUNT_BLOCKS) {
+    if (solved && n_unique != nullptr) {
+      // |unique(idx[valid])| (tracker.py:106-108): popcount of the byte map track_setup wrote (0/1 bytes,
+      // 16-B padded), here after the solve instead of on the first GN iteration's critical path. A few
+      // blocks reduce in LDS and add once each: one device-scope atomic per block, not per wave.
+      __shared__ int s_cnt[4];
+      const uint4* fl = reinterpret_cast<const uint4*>(flags);
+      const int n16 = (N + 15) / 16;
+      int cnt = 0;
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += FUSE_COUNT_BLOCKS * 256) {
+        const uint4 v = fl[i];
+        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+      }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-      if (tot) atomicAdd(n_unique, tot);
+      for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+      if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        if (tot) atomicAdd(n_unique, tot);
+      }
     }
+    if (threadIdx.x == 0 && pub.mirror != nullptr) publish_state(st, pub);
   }
+  if (!solved) return;
   if (f.X_in == nullptr || !(st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)) return;
   if (n >= N) return;
   float T[8];
@@ -654,9 +671,10 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
 // fusion (f->X_in non-null) and/or the unique-match count (count: the state's n_unique from the byte
 // map) for the GN batch chunk_id that finished
 extern "C" hipError_t m3s_launch_fuse(const TrackArgs* a, int chunk_id, const FuseArgs* f, int count, int N,
-                                      hipStream_t s) {
-  hipLaunchKernelGGL(m3s::fuse_kernel, dim3((N + 255) / 256), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
-                     count ? &a->state->n_unique : nullptr);
+                                      const TrackPublish* pub, hipStream_t s) {
+  const int grid = (N + 255) / 256 > FUSE_COUNT_BLOCKS ? (N + 255) / 256 : FUSE_COUNT_BLOCKS;  // every counting block publishes
+  hipLaunchKernelGGL(m3s::fuse_kernel, dim3(grid), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
+                     count ? &a->state->n_unique : nullptr, *pub);
   return hipGetLastError();
 }
 

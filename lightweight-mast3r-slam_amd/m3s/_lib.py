@@ -164,9 +164,12 @@ def ptr(t):
 _WS = {}
 
 
-def workspace(key, nbytes, device):
-    """A cached uint8 device buffer per (key, device), grown on demand (torch caching allocator)."""
-    k = (key, str(device))
+def workspace(key, nbytes, device, stream):
+    """A cached uint8 device buffer per (key, device, stream), grown on demand (torch caching allocator).
+
+    Contract: a buffer is only ever used by launches on the one stream it is keyed by, so consecutive
+    calls reuse it in stream order; calls on another stream get their own buffer."""
+    k = (key, device, stream.value)
     buf = _WS.get(k)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -30,8 +30,6 @@ def _f32(t):
 
 
 def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None):
-    cfg = config["matching"]
-    lib = _lib.load()
     _lib.require_cuda("match", X11, X21, D11, D21, idx_1_to_2_init)
     b, h, w = X21.shape[:3]
     F = D11.shape[-1]
@@ -39,6 +37,27 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None):
     D21 = _f32(D21).reshape(b, h, w, F)
     if tuple(X11.shape) != (b, h, w, 3) or tuple(D11.shape) != (b, h, w, F):
         raise RuntimeError("match: X11/X21 (B,H,W,3) and D11/D21 (B,H,W,F) must agree")
+    return _match(X11.data_ptr(), X21.data_ptr(), D11.data_ptr(), D21.data_ptr(), b, h, w, F, X11.device,
+                  idx_1_to_2_init)
+
+
+def match_halves(X, D, idx_1_to_2_init=None):
+    """``match(X[:b], X[b:], D[:b], D[b:], init)`` for stacked decoder outputs X (2b,H,W,3), D (2b,H,W,F)
+    (mast3r_utils.py:238-240), with the halves passed as pointer offsets instead of four slice tensors."""
+    _lib.require_cuda("match", X, D, idx_1_to_2_init)
+    b2, h, w = X.shape[:3]
+    F = D.shape[-1]
+    X, D = _f32(X), _f32(D)
+    if b2 % 2 or tuple(X.shape) != (b2, h, w, 3) or tuple(D.shape) != (b2, h, w, F):
+        raise RuntimeError("match: X (2B,H,W,3) and D (2B,H,W,F) must agree")
+    b = b2 // 2
+    xp, dp = X.data_ptr(), D.data_ptr()
+    return _match(xp, xp + b * h * w * 3 * 4, dp, dp + b * h * w * F * 4, b, h, w, F, X.device, idx_1_to_2_init)
+
+
+def _match(x11, x21, d11, d21, b, h, w, F, dev, idx_1_to_2_init):
+    cfg = config["matching"]
+    lib = _lib.load()
     init = 0
     if idx_1_to_2_init is not None:
         init_t = idx_1_to_2_init
@@ -47,12 +66,12 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None):
         if init_t.numel() != b * h * w:
             raise RuntimeError("match: idx_1_to_2_init must hold B*H*W indices")
         init = init_t.data_ptr()
-    dev = X11.device
     idx = torch.empty((b, h * w), dtype=torch.int64, device=dev)
     valid = torch.empty((b, h * w, 1), dtype=torch.bool, device=dev)
-    ws = _lib.workspace("match", lib.m3s_match_workspace_size(b, h, w, F), dev)
-    _lib.check(lib.m3s_match(X11.data_ptr(), X21.data_ptr(), D11.data_ptr(), D21.data_ptr(), init, idx.data_ptr(),
-                             valid.data_ptr(), b, h, w, F, int(cfg["max_iter"]), float(cfg["lambda_init"]),
-                             float(cfg["convergence_thresh"]), float(cfg["dist_thresh"]), int(cfg["radius"]),
-                             int(cfg["dilation_max"]), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
+    st = _lib.stream_ptr(dev)
+    ws = _lib.workspace("match", lib.m3s_match_workspace_size(b, h, w, F), dev, st)
+    _lib.check(lib.m3s_match(x11, x21, d11, d21, init, idx.data_ptr(), valid.data_ptr(), b, h, w, F,
+                             int(cfg["max_iter"]), float(cfg["lambda_init"]), float(cfg["convergence_thresh"]),
+                             float(cfg["dist_thresh"]), int(cfg["radius"]), int(cfg["dilation_max"]), ws.data_ptr(),
+                             ws.numel(), st))
     return idx, valid

@@ -54,9 +54,10 @@ class Codebook:
         if not 1 <= k <= 8 or k > self.C:
             raise RuntimeError(f"quantize: multiple_assignment k={k} must be in 1..min(8, C={self.C})")
         nbytes = lib.m3s_quantize_workspace_size(self.C, self.D, M, k)
-        ws = _lib.workspace("quantize", nbytes, self.device)
+        st = _lib.stream_ptr(self.device)
+        ws = _lib.workspace("quantize", nbytes, self.device, st)
         _lib.check(lib.m3s_quantize(_lib.ptr(self._buf), self.C, self.D, _lib.ptr(q), M, k, _lib.ptr(out),
-                                    _lib.ptr(ws), nbytes, _lib.stream_ptr(self.device)))
+                                    _lib.ptr(ws), nbytes, st))
         return out
 
 

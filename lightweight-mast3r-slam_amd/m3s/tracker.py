@@ -17,7 +17,7 @@ import torch
 
 from m3s import _lib
 from m3s.config import config
-from m3s.matching import match
+from m3s.matching import match, match_halves
 from m3s.sim3 import Sim3
 
 
@@ -46,7 +46,7 @@ def mast3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
     X, C, D, Q = asymmetric_inference(model, frame_i, frame_j)
     b = X.shape[0] // 2
     h, w = X.shape[1:3]
-    idx_i2j, valid_match_j = match(X[:b], X[b:], D[:b], D[b:], idx_1_to_2_init=idx_i2j_init)
+    idx_i2j, valid_match_j = match_halves(X, D, idx_1_to_2_init=idx_i2j_init)  # match(X[:b], X[b:], D[:b], D[b:])
     Xr = X.reshape(2 * b, h * w, 3)
     Cr = C.reshape(2 * b, h * w, 1)
     Qr = Q.reshape(2 * b, h * w, 1)
@@ -153,7 +153,7 @@ class FrameTracker:
         # other filtering mode / an empty keyframe goes through keyframe.update_pointmap
         fuse_fused = cfg["filtering_mode"] == "weighted_pointmap" and keyframe.N > 0
 
-        res, T_out = self._run_track(
+        res, T_f, T_r = self._run_track(
             idx=idx_f2k, valid=valid_match_k, Xf=frame.X_canon, Cf=frame.C, Nf=frame.N, Qff=Qff,
             Xk=keyframe.X_canon, Ck=keyframe.C, Nk=keyframe.N, Qkf=Qkf, T_WCf=frame.T_WC, T_WCk=keyframe.T_WC,
             use_calib=use_calib, img_size=img_size, K=K,
@@ -166,9 +166,9 @@ class FrameTracker:
             print(f"Cholesky failed {frame.frame_id}")
             return False, [], True
 
-        # T_out is a fresh (16,) tensor per call, so views need no copy
-        frame.T_WC = Sim3(T_out[:8].view(1, 8))
-        T_CkCf = Sim3(T_out[8:].view(1, 8))
+        # fresh (1, 8) views of this call's output, made before the launch: no copy, no op after the wait
+        frame.T_WC = Sim3(T_f)
+        T_CkCf = Sim3(T_r)
         if fuse_fused:  # X/C fused on the device by m3s_track into new tensors (frame.py:74-77)
             keyframe.X_canon, keyframe.C = self._fused
             keyframe.N += 1
@@ -227,16 +227,17 @@ class FrameTracker:
             fz = _lib.TrackFuse(Xk_canon=dp(Xin), Ck_sum=dp(Cin), Xkf=dp(Xkf_c), Ckf=dp(Ckf_c), Xk_out=dp(Xo),
                                 Ck_out=dp(Co), Cf=dp(Cf), Ck_avg_out=dp(Cka), Cf_avg_out=dp(Cfa),
                                 Nk_new=float(kf.N + 1), Nf=float(Nf or 1))
-        T_out = torch.empty(16, dtype=torch.float32, device=dev)
+        T_out = torch.empty((2, 1, 8), dtype=torch.float32, device=dev)  # T_WCf | T_CkCf
+        T_f, T_r = T_out.unbind(0)
         res = _lib.TrackResult()
-        ws = _lib.workspace("track", lib.m3s_track_workspace_size(N), dev)
+        st = _lib.stream_ptr(dev)
+        ws = _lib.workspace("track", lib.m3s_track_workspace_size(N), dev, st)
         _lib.check(lib.m3s_track(ctypes.byref(ins), ctypes.byref(tc), ctypes.byref(fz), int(self.first_chunk),
-                                 T_out.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(),
-                                 _lib.stream_ptr(dev)))
+                                 T_out.data_ptr(), ctypes.byref(res), ws.data_ptr(), ws.numel(), st))
         self.last_result = res
         if not direct:  # next frame: enqueue as many GN launches as this one needed (+1) before reading back
             self.first_chunk = max(2, min(int(tc.max_iters), res.iters + 1))
-        return res, T_out
+        return res, T_f, T_r
 
     # ------------------------------------------------------------------ reference method surface
     def get_points_poses(self, frame, keyframe, idx_f2k, img_size, use_calib, K=None):
@@ -273,12 +274,12 @@ class FrameTracker:
         n = Xf.shape[0]
         if img_size is None:
             img_size = (1, n)
-        res, T_out = self._run_track(idx=None, valid=valid, Xf=Xf, Cf=None, Nf=1, Qff=Qk.reshape(-1), Xk=Xk, Ck=None,
+        res, T_f, T_r = self._run_track(idx=None, valid=valid, Xf=Xf, Cf=None, Nf=1, Qff=Qk.reshape(-1), Xk=Xk, Ck=None,
                                      Nk=1, Qkf=None, T_WCf=T_WCf, T_WCk=T_WCk, use_calib=use_calib,
                                      img_size=img_size, K=K, direct=True, meas_k=meas_k, valid_meas_k=valid_meas_k)
         if res.status == _lib.TRACK_CHOLESKY_FAILED:
             raise RuntimeError("linalg.cholesky: The factorization could not be completed")
-        return Sim3(T_out[:8].view(1, 8)), Sim3(T_out[8:].view(1, 8))
+        return Sim3(T_f), Sim3(T_r)
 
     def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
         """tracker.py:173-214 -> (T_WCf, T_CkCf)."""

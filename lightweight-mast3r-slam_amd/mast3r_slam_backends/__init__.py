@@ -97,11 +97,12 @@ def _gauss_newton(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, cfg, max
     dev = Twc.device
     dx = torch.zeros((max(Kp - 1, 0), 7), dtype=torch.float32, device=dev)
     nbytes = lib.m3s_ba_workspace_size(Kp, N, E)
-    ws = _lib.workspace("ba", nbytes, dev)
+    st = _lib.stream_ptr(dev)
+    ws = _lib.workspace("ba", nbytes, dev, st)
     _lib.check(lib.m3s_gauss_newton(ctypes.byref(cfg), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs), Kp, N,
                                     _lib.ptr(ii), _lib.ptr(jj), E, _lib.ptr(idx_ii2jj), _lib.ptr(valid_match),
                                     _lib.ptr(Q), int(max_iter), float(delta_thresh), _lib.ptr(dx), None,
-                                    _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)))
+                                    _lib.ptr(ws), ws.numel(), st))
     return [dx]
 
 
