@@ -19,7 +19,7 @@ import sys
 
 src, tag = sys.argv[1], sys.argv[2]
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-out = os.path.join(repo, "profiles")
+out = os.environ.get("PROF_OUT", os.path.join(repo, "profiles"))
 os.makedirs(out, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
 
