@@ -35,7 +35,7 @@ hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, con
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
-hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, hipStream_t);
+hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, hipStream_t);
 hipError_t m3s_launch_ba_solve_dense(const BaArgs*, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
 hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, int, float, float*, hipStream_t);
@@ -441,11 +441,14 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
 // ------------------------------------------------------------------------------------------
 namespace {
 
+constexpr int BA_MAX_WIDE_STEPS = 40;
+
 struct BaPlanImpl {
   BaArgs a;
   BaParams p;
   int Kp, N, E, e0, e1;
   int nL;
+  int step_tasks[BA_MAX_WIDE_STEPS];  // tasks (waves) of each multi-workgroup factor step
   int dense;  // 1: the dense fallback factorisation (ba_dense.hip)
   float delta_thresh;
   size_t edge_sums_off, edge_sums_bytes;
@@ -678,6 +681,22 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     if (!strcmp(f, "sparse")) P.dense = 0;
     if (!strcmp(f, "dense") && P.a.H) P.dense = 1;
   }
+  // factor steps wider than one workgroup's 16 waves run as multi-workgroup launches: every step up to the
+  // last such step (the leaf end of the elimination tree; measured: ~12 rounds of 16 waves per leaf step in
+  // one workgroup), the narrow root end stays in the one-workgroup kernel
+  {
+    int thr = 16;
+    if (const char* w = getenv("M3S_BA_WIDE")) thr = atoi(w);  // experiments: 0 = every step, huge = none
+    int last = -1;
+    for (int l = 0; l <= S.nlev; l++) {
+      const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
+      const int tasks = na + S.grp_ptr[l + 1] - S.grp_ptr[l];
+      if (l < BA_MAX_WIDE_STEPS) P.step_tasks[l] = tasks;
+      if (tasks > thr) last = l;
+    }
+    P.a.wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+  }
+  P.a.bad = P.a.info + 3;
   P.a.plan_lo = reinterpret_cast<const char*>(P.a.col_ptr);
   P.a.plan_bytes = (int)(reinterpret_cast<const char*>(P.a.sidx) + S.sidx.size() * sizeof(int) - P.a.plan_lo);
   P.a.nb = S.nb;
@@ -775,7 +794,7 @@ extern "C" int m3s_ba_solve(const m3s_ba_plan* plan, void* stream) {
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
   Span sp("ba_solve", (hipStream_t)stream);
   HIP_TRY(P->dense ? m3s_launch_ba_solve_dense(&P->a, P->Kp, P->nL, P->delta_thresh, (hipStream_t)stream)
-                   : m3s_launch_ba_solve(&P->a, P->Kp, P->nL, P->delta_thresh, (hipStream_t)stream),
+                   : m3s_launch_ba_solve(&P->a, P->Kp, P->nL, P->delta_thresh, P->step_tasks, (hipStream_t)stream),
           "ba solve launch");
   return M3S_OK;
 }

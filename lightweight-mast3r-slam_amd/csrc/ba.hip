@@ -372,6 +372,7 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL) {
   if (*a.done) return;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
+  if (b == 0 && t == 0) *a.bad = 0;  // the multi-workgroup factor steps of this solve start clean
   const int* ptr = b < nL ? a.asm_ptr + b : a.rhs_ptr + (b - nL);
   const int* ent = b < nL ? a.asm_ent : a.rhs_ent;
   int li;
@@ -477,6 +478,23 @@ struct SpTables {
   const int4* src;
   const int* sidx;
 };
+
+// the loop tables at `base`: the plan's table region [plan_lo, plan_lo + plan_bytes) staged to `base` (LDS), or
+// base = plan_lo itself (global)
+__device__ __forceinline__ SpTables sp_tables(const BaArgs& a, const int* base) {
+  const int* g = reinterpret_cast<const int*>(a.plan_lo);
+  SpTables T;
+  T.col_ptr = base + (a.col_ptr - g);
+  T.rowL = base + (a.rowL - g);
+  T.lev_ptr = base + (a.lev_ptr - g);
+  T.lev_col = base + (a.lev_col - g);
+  T.grp_ptr = base + (a.grp_ptr - g);
+  T.grp = reinterpret_cast<const int4*>(base + (reinterpret_cast<const int*>(a.grp) - g));
+  T.pull_grp = base + (a.pull_grp - g);
+  T.src = reinterpret_cast<const int4*>(base + (reinterpret_cast<const int*>(a.src) - g));
+  T.sidx = base + (a.sidx - g);
+  return T;
+}
 
 // the rows of a column: row p < 7 (noff + 1) is row p % 7 of the column's block p / 7 (block 0 = the
 // diagonal block), row 7 (noff + 1) is the rhs block y_j
@@ -716,6 +734,23 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
   wave_sync();
 }
 
+// One wide factor step l of the elimination tree (its level's factor tasks + the update groups whose sources
+// sit one level below) as a multi-workgroup launch: one wave per task, the same per-task code and therefore
+// the same arithmetic as inside ba_sparse_factor_kernel (bit-identical factor). The launch boundary orders
+// the steps. The leaf end of a minimum-degree tree is wide (one workgroup's 16 waves took ~12 rounds per
+// step there), the root end a chain of single columns, which stays inside the one-workgroup kernel.
+__global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int l) {
+  if (*a.done) return;
+  __shared__ double s_red[64];
+  const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
+  const int lane = threadIdx.x;
+  const int task = blockIdx.x;
+  const int c0 = l < a.nlev ? T.lev_ptr[l] : 0, na = l < a.nlev ? T.lev_ptr[l + 1] - c0 : 0;
+  const int t0 = T.grp_ptr[l], nt = T.grp_ptr[l + 1] - t0;
+  if (task < na) sp_factor_column(a, T, T.lev_col[c0 + task], lane, s_red, a.bad);
+  else if (task < na + nt) sp_update_group(a, T, t0 + task - na, lane, s_red);
+}
+
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
 __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
@@ -744,23 +779,14 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   const int* base = LT ? static_cast<const int*>(s_plan) : g;
   double* X = LT ? reinterpret_cast<double*>(s_plan + xoff) : a.xs;
-  SpTables T;
-  T.col_ptr = base + (a.col_ptr - g);
-  T.rowL = base + (a.rowL - g);
-  T.lev_ptr = base + (a.lev_ptr - g);
-  T.lev_col = base + (a.lev_col - g);
-  T.grp_ptr = base + (a.grp_ptr - g);
-  T.grp = reinterpret_cast<const int4*>(base + (reinterpret_cast<const int*>(a.grp) - g));
-  T.pull_grp = base + (a.pull_grp - g);
-  T.src = reinterpret_cast<const int4*>(base + (reinterpret_cast<const int*>(a.src) - g));
-  T.sidx = base + (a.sidx - g);
+  const SpTables T = sp_tables(a, base);
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   SPST(1);
   // step l: factor the columns of level l (each pulls its children's-level updates first) beside the
   // push updates of level l-1 into the columns above level l
   const int nlev = a.nlev;
-  for (int l = 0; l <= nlev; l++) {
+  for (int l = a.wide_steps; l <= nlev; l++) {
     const int c0 = l < nlev ? T.lev_ptr[l] : 0, na = l < nlev ? T.lev_ptr[l + 1] - c0 : 0;
     const int t0 = T.grp_ptr[l], nt = T.grp_ptr[l + 1] - t0;
     for (int task = w; task < na + nt; task += SP_WAVES) {
@@ -783,7 +809,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   __syncthreads();
   SPST(3 + 2 * nlev);
-  const bool failed = s_bad != 0;
+  const bool failed = s_bad != 0 || (a.wide_steps > 0 && *a.bad != 0);
   const int n = a.nb * 7;
   float n2 = 0.0f;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -850,8 +876,11 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 }
 
 // assembly (nL factor blocks + nb rhs rows), then the one-workgroup factor / solve / retraction
-extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, hipStream_t s) {
+extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, const int* step_tasks,
+                                          hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
+  for (int l = 0; l < a->wide_steps; l++)
+    if (step_tasks[l] > 0) hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, l);
   if (((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 <= (size_t)m3s::SP_PLAN_BYTES)
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else

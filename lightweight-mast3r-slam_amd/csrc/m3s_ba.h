@@ -35,6 +35,7 @@ struct BaArgs {
   // block-sparse pose system (ba_pattern.h; analysed once per plan, factored on the device every iteration)
   int nb;                 // block columns = poses - 1 (pin)
   int nlev;               // elimination-tree levels
+  int wide_steps;         // factor steps [0, wide_steps) run as multi-workgroup launches (ba_sparse_step_kernel)
   const int* perm;        // (nb) factor column -> pose index (pin removed)
   const int* col_ptr;     // (nb+1) factor blocks of each column, diagonal first
   const int* rowL;        // (nL) block row of each factor block
@@ -60,4 +61,5 @@ struct BaArgs {
   int* info;   // factorisation failure flag
   int* done;   // early-exit flag (|dx| < delta_thresh)
   int* iters;  // iterations executed
+  int* bad;    // non-positive pivot seen by a multi-workgroup factor step (cleared by the assembly)
 };

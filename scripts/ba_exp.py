@@ -60,7 +60,9 @@ for rep in range(2):
         _lib.check(lib.m3s_timing_query(name.encode(), ms, cnt))
         out[name] = ms.value / max(cnt.value, 1)
     gb = E * H * W * 45 / 1e6  # MB -> MB/ms = GB/s
-    print(f"rep {rep}: E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
+    import hashlib
+    twc_hash = hashlib.sha1(Twc.cpu().numpy().tobytes()).hexdigest()[:12]
+    print(f"rep {rep}: Twc sha1 {twc_hash} E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
           f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}", flush=True)
 
 
