@@ -163,7 +163,11 @@ __device__ __forceinline__ bool track_skipped(unsigned n_valid_opt, const TrackP
   return (float)n_valid_opt / (float)p.N < p.min_match_frac;  // tracker.py:67-70
 }
 
-// accumulate one whitened row (tracker.py:156-166): robust = si*sqrt(huber(si*r)); A = robust*J; b = robust*r
+// accumulate one whitened row (tracker.py:156-166): robust = si*sqrt(huber(si*r)); A = robust*J; b = robust*r.
+// MASK: the row's structurally nonzero Jacobian entries (bit c; the calib rows of chain_row have constant
+// -0 entries): their products add an exact +-0 to the fp64 sums and are skipped (a non-finite row still
+// turns the structurally nonzero entries into NaN, so a failing solve still fails).
+template <unsigned MASK = 0x7fu>
 __device__ __forceinline__ void acc_row(double* acc, const float J[7], float r, float si, float k) {
   const float wr = si * r;
   const float ra = fabsf(wr);
@@ -177,10 +181,14 @@ __device__ __forceinline__ void acc_row(double* acc, const float J[7], float r, 
 #pragma unroll
   for (int c = 0; c < 7; c++) {
 #pragma unroll
-    for (int d = c; d < 7; d++) acc[l++] += (double)A[c] * (double)A[d];
+    for (int d = c; d < 7; d++) {
+      if ((MASK >> c) & (MASK >> d) & 1u) acc[l] += (double)A[c] * (double)A[d];
+      l++;
+    }
   }
 #pragma unroll
-  for (int c = 0; c < 7; c++) acc[28 + c] -= (double)A[c] * (double)b;  // g = -A^T b
+  for (int c = 0; c < 7; c++)
+    if ((MASK >> c) & 1u) acc[28 + c] -= (double)A[c] * (double)b;  // g = -A^T b
   acc[35] += 0.5 * (double)b * (double)b;
 }
 
@@ -369,17 +377,17 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
     dh[1] = 0.0f;
     dh[2] = (-p.K[0] * x * zi) * zi;
     chain_row(dh, Y, J);
-    acc_row(acc, J, res[0], si_p, p.huber_k);
+    acc_row<0b1111101u>(acc, J, res[0], si_p, p.huber_k);  // J[1] = -dh[1] = -0
     dh[0] = 0.0f;
     dh[1] = p.K[4] * zi;
     dh[2] = (-p.K[4] * y * zi) * zi;
     chain_row(dh, Y, J);
-    acc_row(acc, J, res[1], si_p, p.huber_k);
+    acc_row<0b1111110u>(acc, J, res[1], si_p, p.huber_k);  // J[0] = -0
     dh[0] = 0.0f;
     dh[1] = 0.0f;
     dh[2] = zi;
     chain_row(dh, Y, J);
-    acc_row(acc, J, res[2], si_z, p.huber_k);
+    acc_row<0b1011100u>(acc, J, res[2], si_z, p.huber_k);  // J[0], J[1], J[5] = -0
   }
 }
 
@@ -418,6 +426,16 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   for (int c = 0; c < 8; c++) T[c] = st->T[c];
   const float4* rec = reinterpret_cast<const float4*>(a.rec);
   const int stride = gridDim.x * GN_THREADS;
+  // the first round's records (every point at 512x512: 4 per thread) stay in registers for all iterations;
+  // only the poses change between iterations
+  const int n00 = blockIdx.x * GN_THREADS + threadIdx.x;
+  float4 c0[GN_PPT], c1[GN_PPT];
+#pragma unroll
+  for (int u = 0; u < GN_PPT; u++) {
+    const int n = min(n00 + u * stride, p.N - 1);
+    c0[u] = rec[2 * (size_t)n];
+    c1[u] = rec[2 * (size_t)n + 1];
+  }
   for (int it = 0; it < p.max_iters; it++) {
 #ifdef M3S_GN_STAMPS
     const int iter0 = it;
@@ -426,7 +444,10 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     double acc[GN_NSUM];
 #pragma unroll
     for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
-    for (int n0 = blockIdx.x * GN_THREADS + threadIdx.x; n0 < p.N; n0 += GN_PPT * stride) {
+#pragma unroll
+    for (int u = 0; u < GN_PPT; u++)
+      if (n00 + u * stride < p.N) gn_point(p, T, c0[u], c1[u], acc);
+    for (int n0 = n00 + GN_PPT * stride; n0 < p.N; n0 += GN_PPT * stride) {
       float4 r0[GN_PPT], r1[GN_PPT];
 #pragma unroll
       for (int u = 0; u < GN_PPT; u++) {
