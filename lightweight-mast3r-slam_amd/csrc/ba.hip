@@ -32,59 +32,75 @@ namespace m3s {
 // ------------------------------------------------------------------------------------------
 // linearisation
 // ------------------------------------------------------------------------------------------
-// MASK: the row's structurally nonzero Jacobian entries (bit c). Products with a structural zero
-// are skipped: for finite weights they add an exact +-0 to the sum, so the result is unchanged
-// (the reference computes them; ~45% of the FMAs in rays mode).
-// BA_RUN_LEN > 0: products and sums in fp32 over runs of BA_RUN_LEN points per lane, each run added to the
-// fp64 accumulators (packed fp32 FMAs instead of fp64 ones: the kernel is VALU-issue bound); 0: products
-// and sums in fp64 from the fp32 rows.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// MASK: the row's structurally nonzero Jacobian entries (bit c). Products with a structural zero are skipped:
+// for finite weights they add an exact +-0 to the sum, so the result is unchanged (the reference computes
+// them; ~45% of the FMAs in rays mode). Products and sums in fp32 (packed: two points per instruction) over
+// runs of BA_RUN_LEN rounds per slot, each run then added to the fp64 accumulators (the kernel is VALU-issue
+// bound; fp64 products put no measurable accuracy gain against the fp64 truth once runs are short).
 #ifndef BA_RUN_LEN
 #define BA_RUN_LEN 4
 #endif
 template <unsigned MASK>
-__device__ __forceinline__ void acc_local(double* L, double* v, const float J[7], float w, float e) {
-  double Jd[7];
-#pragma unroll
-  for (int c = 0; c < 7; c++) Jd[c] = (double)J[c];
-  const double wd = (double)w, ed = (double)e;
+__device__ __forceinline__ void acc_local_f2(f2* L, f2* v, const f2 J[7], f2 w, f2 e) {
   int l = 0;
 #pragma unroll
   for (int c = 0; c < 7; c++) {
-    const double wj = wd * Jd[c];
+    const f2 wj = w * J[c];
 #pragma unroll
     for (int d = c; d < 7; d++) {
-      if ((MASK >> c) & (MASK >> d) & 1u) L[l] += wj * Jd[d];
+      if ((MASK >> c) & (MASK >> d) & 1u) L[l] = __builtin_elementwise_fma(wj, J[d], L[l]);
       l++;
     }
-    if ((MASK >> c) & 1u) v[c] += wj * ed;
+    if ((MASK >> c) & 1u) v[c] = __builtin_elementwise_fma(wj, e, v[c]);
   }
 }
 
-template <unsigned MASK>
-__device__ __forceinline__ void acc_local_f32(float* L, float* v, const float J[7], float w, float e) {
-  int l = 0;
-#pragma unroll
-  for (int c = 0; c < 7; c++) {
-    const float wj = w * J[c];
-#pragma unroll
-    for (int d = c; d < 7; d++) {
-      if ((MASK >> c) & (MASK >> d) & 1u) L[l] = fmaf(wj, J[d], L[l]);
-      l++;
-    }
-    if ((MASK >> c) & 1u) v[c] = fmaf(wj, e, v[c]);
-  }
+// huber weight (gn_kernels.cu:172-175, k = 1.345 as a double) of two residuals. The reference's quotient is
+// the double division k / |r| rounded to float; here the float quotient of the two-float k = KH + KL by |r|,
+// refined by one FMA residual step (equal to the double route but for a rounding tie within ~2^-48), so no
+// fp64 division sequence runs for every row (the select evaluated it unconditionally).
+__device__ __forceinline__ f2 huber_ba2(f2 r) {
+  constexpr float KH = 1.345f;
+  constexpr float KL = (float)(1.345 - (double)1.345f);
+  const f2 ra = {fabsf(r.x), fabsf(r.y)};
+  const f2 y = {__builtin_amdgcn_rcpf(ra.x), __builtin_amdgcn_rcpf(ra.y)};
+  const f2 q0 = KH * y;
+  const f2 e = __builtin_elementwise_fma(-q0, ra, f2{KH, KH}) + KL;
+  const f2 q = __builtin_elementwise_fma(e, y, q0);
+  return ra < KH ? f2{1.0f, 1.0f} : q;
 }
 
-#ifndef BA_PPT  // points per lane per round of the linearisation loop (loads first)
-#define BA_PPT 2
+// 1/sqrt(x) and 1/x of two values: the hardware estimates (~1 ulp), with BA_RAYS_NEWTON one Newton step each
+// (packed), which takes out the estimates' bias against the reference's IEEE sqrtf and divisions
+__device__ __forceinline__ f2 rsq2(f2 x) {
+  f2 y = {__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)};
+#ifdef BA_RAYS_NEWTON
+  y = y * __builtin_elementwise_fma(-0.5f * x * y, y, f2{1.5f, 1.5f});
 #endif
+  return y;
+}
+__device__ __forceinline__ f2 rcp2(f2 x) {
+  f2 y = {__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
+#ifdef BA_RAYS_NEWTON
+  y = y * __builtin_elementwise_fma(-x, y, f2{2.0f, 2.0f});
+#endif
+  return y;
+}
+
+// actSO3 of two points (component arrays), same expression as actSO3
+__device__ __forceinline__ void actSO3_v(const float* q, const f2* X, f2* Y) {
+  const f2 uv0 = 2.0f * (q[1] * X[2] - q[2] * X[1]);
+  const f2 uv1 = 2.0f * (q[2] * X[0] - q[0] * X[2]);
+  const f2 uv2 = 2.0f * (q[0] * X[1] - q[1] * X[0]);
+  Y[0] = X[0] + q[3] * uv0 + (q[1] * uv2 - q[2] * uv1);
+  Y[1] = X[1] + q[3] * uv1 + (q[2] * uv0 - q[0] * uv2);
+  Y[2] = X[2] + q[3] * uv2 + (q[0] * uv1 - q[1] * uv0);
+}
+
 #ifndef BA_LIN_WAVES  // waves per SIMD the linearisation is compiled for (VGPR budget 512 / waves)
-#define BA_LIN_WAVES (BA_RUN_LEN > 0 ? 3 : 4)
-#endif
-#if BA_RUN_LEN > 0
-#define ACC_ROW(MASK, J, W, E) acc_local_f32<MASK>(fL, fv, J, W, E)
-#else
-#define ACC_ROW(MASK, J, W, E) acc_local<MASK>(L, v, J, W, E)
+#define BA_LIN_WAVES 2
 #endif
 
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
@@ -146,124 +162,121 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
   const int k_end = min(N, k_begin + per);
-#if BA_RUN_LEN > 0
-  float fL[28], fv[7];
+  f2 fL[28], fv[7];  // fp32 run sums, one slot per point of the pair
 #pragma unroll
-  for (int c = 0; c < 28; c++) fL[c] = 0.0f;
+  for (int c = 0; c < 28; c++) fL[c] = f2{0.0f, 0.0f};
 #pragma unroll
-  for (int c = 0; c < 7; c++) fv[c] = 0.0f;
+  for (int c = 0; c < 7; c++) fv[c] = f2{0.0f, 0.0f};
   int run = 0;
-#endif
-  // BA_PPT points per lane per round: every round's record / Xj loads are issued before its math
-  for (int k0 = k_begin + threadIdx.x; k0 < k_end; k0 += BA_PPT * blockDim.x) {
-    float4 Rr[BA_PPT];
-    float Xjr[BA_PPT][3];
+  // two points per lane per round, (k0, k0 + blockDim): every per-point float operation runs on both at once
+  // as one packed fp32 instruction (v_pk_fma/mul/add_f32; float2 lanes), the transcendentals per component
+  for (int k0 = k_begin + threadIdx.x; k0 < k_end; k0 += 2 * blockDim.x) {
+    const int k1 = k0 + (int)blockDim.x;
+    const bool has1 = k1 < k_end;
+    // a missing second point repeats the first with weight 0: it adds exact zeros unless the first point's own
+    // row is non-finite, which poisons the sums anyway (another point as filler changed the rays sums)
+    const int k1c = has1 ? k1 : k0;
+    const float4 R0 = rec[k0], R1 = rec[k1c];
+    f2 Xj[3];
 #pragma unroll
-    for (int u = 0; u < BA_PPT; u++) {
-      const int k = min(k0 + u * (int)blockDim.x, k_end - 1);
-      Rr[u] = rec[k];
+    for (int c = 0; c < 3; c++) Xj[c] = f2{Xj_base[(size_t)k0 * 3 + c], Xj_base[(size_t)k1c * 3 + c]};
+    const f2 Rx = {R0.x, R1.x}, Ry = {R0.y, R1.y}, Rz = {R0.z, R1.z};
+    // sqrt(q), 0 for an invalid match (ba_pack) and for the missing second point of a ragged tail
+    const f2 sqq = {R0.w, has1 ? R1.w : 0.0f};
+    f2 Y[3];
+    actSO3_v(&Tij[3], Xj, Y);  // actSim3 (gn_kernels.cu:207-219): rotate, scale, translate
 #pragma unroll
-      for (int c = 0; c < 3; c++) Xjr[u][c] = Xj_base[(size_t)k * 3 + c];
-    }
-#pragma unroll
-    for (int u = 0; u < BA_PPT; u++) {
-    if (k0 + u * (int)blockDim.x >= k_end) break;
-    const float4 R = Rr[u];
-    const float Xj[3] = {Xjr[u][0], Xjr[u][1], Xjr[u][2]};
-    float Y[3];
-    actSO3(&Tij[3], Xj, Y);  // actSim3 (gn_kernels.cu:207-219): rotate, scale, translate
-    Y[0] = Y[0] * Tij[7];
-    Y[1] = Y[1] * Tij[7];
-    Y[2] = Y[2] * Tij[7];
-    Y[0] += Tij[0];
-    Y[1] += Tij[1];
-    Y[2] += Tij[2];
-    const float sqq = R.w;  // sqrt(q), 0 for an invalid match (ba_pack)
+    for (int c = 0; c < 3; c++) Y[c] = Y[c] * Tij[7] + Tij[c];
     if constexpr (MODE == BA_MODE_POINTS) {
-      const float Xi[3] = {R.x, R.y, R.z};
-      const float err[3] = {Y[0] - Xi[0], Y[1] - Xi[1], Y[2] - Xi[2]};
-      const float sw = p.inv_a * sqq;
-      const float wc = sw * sw;
-      const float J0[7] = {1.0f, 0.0f, 0.0f, 0.0f, Y[2], -Y[1], Y[0]};
-      const float J1[7] = {0.0f, 1.0f, 0.0f, -Y[2], 0.0f, Y[0], Y[1]};
-      const float J2[7] = {0.0f, 0.0f, 1.0f, Y[1], -Y[0], 0.0f, Y[2]};
-      ACC_ROW(0b1110001, J0, huber_ba(sw * err[0]) * wc, err[0]);  // {0,4,5,6}
-      ACC_ROW(0b1101010, J1, huber_ba(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
-      ACC_ROW(0b1011100, J2, huber_ba(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
+      const f2 err[3] = {Y[0] - Rx, Y[1] - Ry, Y[2] - Rz};
+      const f2 sw = p.inv_a * sqq;
+      const f2 wc = sw * sw;
+      const f2 z2 = {0.0f, 0.0f}, o2 = {1.0f, 1.0f};
+      const f2 J0[7] = {o2, z2, z2, z2, Y[2], -Y[1], Y[0]};
+      const f2 J1[7] = {z2, o2, z2, -Y[2], z2, Y[0], Y[1]};
+      const f2 J2[7] = {z2, z2, o2, Y[1], -Y[0], z2, Y[2]};
+      acc_local_f2<0b1110001>(fL, fv, J0, huber_ba2(sw * err[0]) * wc, err[0]);  // {0,4,5,6}
+      acc_local_f2<0b1101010>(fL, fv, J1, huber_ba2(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
+      acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
     } else if constexpr (MODE == BA_MODE_RAYS) {
-      const float Xi[3] = {R.x, R.y, R.z};
-      const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
-      const float n1i_inv = __builtin_amdgcn_rsqf(n2i);
-      const float n1i = n2i * n1i_inv;
-      const float n2j = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
-      const float n1j_inv = __builtin_amdgcn_rsqf(n2j);
-      const float n1j = n2j * n1j_inv;
-      const float rj[3] = {n1j_inv * Y[0], n1j_inv * Y[1], n1j_inv * Y[2]};
-      const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1], rj[2] - n1i_inv * Xi[2], n1j - n1i};
-      const float swr = p.inv_a * sqq;
-      const float swd = p.inv_b * sqq;
-      const float wr = swr * swr, wd = swd * swd;
-      const float n3 = n1j_inv * __builtin_amdgcn_rcpf(n2j);
-      const float dxx = n1j_inv - Y[0] * Y[0] * n3;
-      const float dyy = n1j_inv - Y[1] * Y[1] * n3;
-      const float dzz = n1j_inv - Y[2] * Y[2] * n3;
-      const float dxy = -Y[0] * Y[1] * n3;
-      const float dxz = -Y[0] * Y[2] * n3;
-      const float dyz = -Y[1] * Y[2] * n3;
-      const float J0[7] = {dxx, dxy, dxz, 0.0f, rj[2], -rj[1], 0.0f};
-      const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.0f, rj[0], 0.0f};
-      const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.0f, 0.0f};
-      const float J3[7] = {rj[0], rj[1], rj[2], 0.0f, 0.0f, 0.0f, n1j};
-      ACC_ROW(0b0110111, J0, huber_ba(swr * err[0]) * wr, err[0]);  // {0,1,2,4,5}
-      ACC_ROW(0b0101111, J1, huber_ba(swr * err[1]) * wr, err[1]);  // {0,1,2,3,5}
-      ACC_ROW(0b0011111, J2, huber_ba(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
-      ACC_ROW(0b1000111, J3, huber_ba(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
+      const f2 n2i = Rx * Rx + Ry * Ry + Rz * Rz;
+      const f2 n1i_inv = rsq2(n2i);
+      const f2 n1i = n2i * n1i_inv;
+      const f2 n2j = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
+      const f2 n1j_inv = rsq2(n2j);
+      const f2 n1j = n2j * n1j_inv;
+      const f2 rj[3] = {n1j_inv * Y[0], n1j_inv * Y[1], n1j_inv * Y[2]};
+      const f2 err[4] = {rj[0] - n1i_inv * Rx, rj[1] - n1i_inv * Ry, rj[2] - n1i_inv * Rz, n1j - n1i};
+      const f2 swr = p.inv_a * sqq;
+      const f2 swd = p.inv_b * sqq;
+      const f2 wr = swr * swr, wd = swd * swd;
+      const f2 n3 = n1j_inv * rcp2(n2j);
+      const f2 dxx = n1j_inv - Y[0] * Y[0] * n3;
+      const f2 dyy = n1j_inv - Y[1] * Y[1] * n3;
+      const f2 dzz = n1j_inv - Y[2] * Y[2] * n3;
+      const f2 dxy = -Y[0] * Y[1] * n3;
+      const f2 dxz = -Y[0] * Y[2] * n3;
+      const f2 dyz = -Y[1] * Y[2] * n3;
+      const f2 z2 = {0.0f, 0.0f};
+      const f2 J0[7] = {dxx, dxy, dxz, z2, rj[2], -rj[1], z2};
+      const f2 J1[7] = {dxy, dyy, dyz, -rj[2], z2, rj[0], z2};
+      const f2 J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], z2, z2};
+      const f2 J3[7] = {rj[0], rj[1], rj[2], z2, z2, z2, n1j};
+      acc_local_f2<0b0110111>(fL, fv, J0, huber_ba2(swr * err[0]) * wr, err[0]);  // {0,1,2,4,5}
+      acc_local_f2<0b0101111>(fL, fv, J1, huber_ba2(swr * err[1]) * wr, err[1]);  // {0,1,2,3,5}
+      acc_local_f2<0b0011111>(fL, fv, J2, huber_ba2(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
+      acc_local_f2<0b1000111>(fL, fv, J3, huber_ba2(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
-      const float u_t = R.x, v_t = R.y, zi = R.z;
-      const bool valid_z = (Y[2] > p.z_eps) && (zi > p.z_eps);
-      const float zj_inv = valid_z ? __builtin_amdgcn_rcpf(Y[2]) : 0.0f;
-      const float zj_log = valid_z ? __logf(Y[2]) : 0.0f;
-      const float zi_log = valid_z ? __logf(zi) : 0.0f;
-      const float xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
-      const float u = p.fx * xz + p.cx, vv = p.fy * yz + p.cy;
-      const bool valid_u = (u > (float)p.pixel_border) && (u < (float)(p.W - 1 - p.pixel_border));
-      const bool valid_v = (vv > (float)p.pixel_border) && (vv < (float)(p.H - 1 - p.pixel_border));
-      const bool valid = valid_u && valid_v && valid_z;
-      const float err[3] = {u - u_t, vv - v_t, zj_log - zi_log};
-      const float swp = valid ? p.inv_a * sqq : 0.0f;
-      const float swd = valid ? p.inv_b * sqq : 0.0f;
-      const float wp = swp * swp, wd = swd * swd;
+      const f2 u_t = Rx, v_t = Ry, zi = Rz;
+      const auto valid_z = (Y[2] > p.z_eps) & (zi > p.z_eps);
+      const f2 z2 = {0.0f, 0.0f};
+      const f2 zj_inv = valid_z ? f2{__builtin_amdgcn_rcpf(Y[2].x), __builtin_amdgcn_rcpf(Y[2].y)} : z2;
+      const f2 zj_log = valid_z ? f2{__logf(Y[2].x), __logf(Y[2].y)} : z2;
+      const f2 zi_log = valid_z ? f2{__logf(zi.x), __logf(zi.y)} : z2;
+      const f2 xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
+      const f2 u = p.fx * xz + p.cx, vv = p.fy * yz + p.cy;
+      const float ub = (float)p.pixel_border, uh = (float)(p.W - 1 - p.pixel_border),
+                  vh = (float)(p.H - 1 - p.pixel_border);
+      const auto valid = (u > ub) & (u < uh) & (vv > ub) & (vv < vh) & valid_z;
+      const f2 err[3] = {u - u_t, vv - v_t, zj_log - zi_log};
+      const f2 swp = valid ? p.inv_a * sqq : z2;
+      const f2 swd = valid ? p.inv_b * sqq : z2;
+      const f2 wp = swp * swp, wd = swd * swd;
       const float fx = p.fx, fy = p.fy;
-      const float J0[7] = {fx * zj_inv, 0.0f, -fx * xz * zj_inv, -fx * xz * yz, fx * (1 + xz * xz), -fx * yz, 0.0f};
-      const float J1[7] = {0.0f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1 + yz * yz), fy * xz * yz, fy * xz, 0.0f};
-      const float J2[7] = {0.0f, 0.0f, zj_inv, yz, -xz, 0.0f, 1.0f};
-      ACC_ROW(0b0111101, J0, huber_ba(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
-      ACC_ROW(0b0111110, J1, huber_ba(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
-      ACC_ROW(0b1011100, J2, huber_ba(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
+      const f2 o2 = {1.0f, 1.0f};
+      const f2 J0[7] = {fx * zj_inv, z2, -fx * xz * zj_inv, -fx * xz * yz, fx * (o2 + xz * xz), -fx * yz, z2};
+      const f2 J1[7] = {z2, fy * zj_inv, -fy * yz * zj_inv, -fy * (o2 + yz * yz), fy * xz * yz, fy * xz, z2};
+      const f2 J2[7] = {z2, z2, zj_inv, yz, -xz, z2, o2};
+      acc_local_f2<0b0111101>(fL, fv, J0, huber_ba2(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
+      acc_local_f2<0b0111110>(fL, fv, J1, huber_ba2(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
+      acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
-    }  // u
-#if BA_RUN_LEN > 0
-    if (++run == BA_RUN_LEN) {  // the run's fp32 sums into the fp64 accumulators
+    if (++run == BA_RUN_LEN) {  // the run's fp32 sums (BA_RUN_LEN points per slot) into the fp64 accumulators
       run = 0;
 #pragma unroll
       for (int c = 0; c < 28; c++) {
-        L[c] += (double)fL[c];
-        fL[c] = 0.0f;
+        L[c] += (double)fL[c].x;
+        L[c] += (double)fL[c].y;
+        fL[c] = f2{0.0f, 0.0f};
       }
 #pragma unroll
       for (int c = 0; c < 7; c++) {
-        v[c] += (double)fv[c];
-        fv[c] = 0.0f;
+        v[c] += (double)fv[c].x;
+        v[c] += (double)fv[c].y;
+        fv[c] = f2{0.0f, 0.0f};
       }
     }
-#endif
   }
-#if BA_RUN_LEN > 0
 #pragma unroll
-  for (int c = 0; c < 28; c++) L[c] += (double)fL[c];
+  for (int c = 0; c < 28; c++) {
+    L[c] += (double)fL[c].x;
+    L[c] += (double)fL[c].y;
+  }
 #pragma unroll
-  for (int c = 0; c < 7; c++) v[c] += (double)fv[c];
-#endif
+  for (int c = 0; c < 7; c++) {
+    v[c] += (double)fv[c].x;
+    v[c] += (double)fv[c].y;
+  }
   // wave64 butterfly in fp64, then 4 waves through LDS
   __shared__ double s_part[4][BA_NSUM];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
