@@ -486,31 +486,37 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     __syncthreads();
     if (s_last) {
       GN_STAMP(3);
-      // last arriver: acquire (invalidates this CU's L1), thread r loads partial row r of this iteration's
-      // slot (no L2 has held it in this launch) as 16-B vectors in one round trip, then the deterministic LDS
-      // reduction; past GN_SLOTS - 1 iterations the last slot is reused and read with sc1 loads
+      // last arriver: acquire (invalidates this CU's L1); thread (c, g) sums column c of the partial rows g,
+      // g + 7, ... straight from this iteration's slot (no L2 has held it in this launch), all 37 loads in
+      // flight at once: the same fixed order as block_sum36 (whose rows beyond the grid are zeros), without its
+      // LDS transpose. Past GN_SLOTS - 1 iterations the last slot is reused and read with sc1 loads.
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      double v[GN_NSUM];
-      if ((int)threadIdx.x < (int)gridDim.x) {
-        if (it < GN_SLOTS - 1) {
-          const double2* row = reinterpret_cast<const double2*>(a.partials + ((size_t)slot * GN_THREADS + threadIdx.x) *
-                                                                                 GN_PSTRIDE);
+      static_assert(GN_THREADS == 256, "the unrolled column walk below assumes 256 partial rows");
+      if (threadIdx.x < 7 * GN_NSUM) {
+        const int c = threadIdx.x % GN_NSUM, g = threadIdx.x / GN_NSUM;
+        const int nrow = (int)gridDim.x;
+        const bool fresh = it < GN_SLOTS - 1;
+        const gdouble* col = part + c;
+        auto ld = [&](int r) -> double {
+          if (r >= nrow) return 0.0;
+          return fresh ? col[(size_t)r * GN_PSTRIDE]
+                       : __hip_atomic_load(&col[(size_t)r * GN_PSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-          for (int c = 0; c < GN_NSUM / 2; c++) {
-            const double2 t = row[c];
-            v[2 * c] = t.x;
-            v[2 * c + 1] = t.y;
-          }
-        } else {
-          const gdouble* row = part + (size_t)threadIdx.x * GN_PSTRIDE;
-#pragma unroll
-          for (int c = 0; c < GN_NSUM; c++) v[c] = __hip_atomic_load(&row[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 18; k++) {  // rows g + 14k (a0) and g + 14k + 7 (a1), all < 256
+          a0 += ld(g + 14 * k);
+          a1 += ld(g + 14 * k + 7);
         }
-      } else {
-#pragma unroll
-        for (int c = 0; c < GN_NSUM; c++) v[c] = 0.0;
+        if (g < 4) a0 += ld(g + 252);
+        s_grp[g][c] = a0 + a1;
       }
-      block_sum36(v, s_all, s_grp, s_sum);
+      __syncthreads();
+      if (threadIdx.x < GN_NSUM) {
+        const int c = threadIdx.x;
+        s_sum[c] = (((((s_grp[0][c] + s_grp[1][c]) + s_grp[2][c]) + s_grp[3][c]) + s_grp[4][c]) + s_grp[5][c]) +
+                   s_grp[6][c];
+      }
       __syncthreads();
       GN_STAMP(4);
       if (threadIdx.x == 0) {
