@@ -384,6 +384,8 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   if (p.mode == 1) M3S_CHECK(p.fx != 0.0f && p.fy != 0.0f, "track: calib mode needs K");
   hipStream_t s = (hipStream_t)stream;
   a.T_out = T_out_dev;
+  a.T_WCf = in->T_WCf;
+  a.T_WCk = in->T_WCk;
   const bool do_fuse = fuse && fuse->Xk_canon;
   FuseArgs fa{};
   if (do_fuse) {

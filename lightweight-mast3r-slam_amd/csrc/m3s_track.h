@@ -58,6 +58,8 @@ struct TrackArgs {
   unsigned* tick;              // (11 x 32) GN arrival tickets: 8 shards + the top counter, one 128-B line each,
                                // then the GnBcast record (two lines)
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
+  const float* T_WCf;          // (8) the frame's pose estimate (device), read by track_setup's state init
+  const float* T_WCk;          // (8) the keyframe's pose (device)
 };
 
 // Per-iteration broadcast of the persistent GN launch, written write-through (sc1) by the block that

@@ -61,15 +61,17 @@ __device__ __forceinline__ void sim3_inv(const float* A, float* C) {
   C[7] = si;
 }
 
-// state <- {0, T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}; the grid zeroes
-// the unique-idx byte map (replaces two memsets + a one-lane launch)
-__global__ void __launch_bounds__(256) track_init_kernel(TrackState* st, const float* T_WCf, const float* T_WCk,
-                                                         uint4* flags, int n16, unsigned long long* cnt, unsigned* tick) {
+// the grid zeroes the unique-idx byte map, the setup counters and the GN tickets / broadcast record (the state
+// itself is initialised by track_setup's first thread: nothing reads it before the GN launch)
+__global__ void __launch_bounds__(256) track_init_kernel(uint4* flags, int n16, unsigned long long* cnt, unsigned* tick) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) flags[i] = make_uint4(0u, 0u, 0u, 0u);
   if (i < M3S_TRACK_SHARDS * 16) cnt[i] = 0ull;
   for (int j = i; j < M3S_TRACK_TICK_WORDS; j += gridDim.x * blockDim.x) tick[j] = 0u;  // tickets + GnBcast
-  if (i != 0) return;
+}
+
+// state <- {0, T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}
+__device__ void track_state_init(TrackState* st, const float* T_WCf, const float* T_WCk) {
   *st = TrackState{};
   float Ti[8], Tf[8], Tk[8];
   for (int c = 0; c < 8; c++) {
@@ -85,6 +87,7 @@ __global__ void __launch_bounds__(256) track_init_kernel(TrackState* st, const f
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n == 0) track_state_init(a.state, a.T_WCf, a.T_WCk);
   int v_opt = 0, v_kf = 0;
   if (n < p.N && p.direct) {  // opt_pose_* surface: Qff = Qk, valid_match = valid, Xf pre-gathered
     const float qk = a.Qff[n];
@@ -675,7 +678,9 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
 extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_WCf, const float* T_WCk, int N,
                                             hipStream_t s) {
   const int n16 = (N + 15) / 16;  // the byte map is carved with a 16-B padded length
-  hipLaunchKernelGGL(m3s::track_init_kernel, dim3((n16 + 255) / 256), dim3(256), 0, s, a->state, T_WCf, T_WCk,
+  (void)T_WCf;
+  (void)T_WCk;  // read by track_setup (TrackArgs)
+  hipLaunchKernelGGL(m3s::track_init_kernel, dim3((n16 + 255) / 256), dim3(256), 0, s,
                      reinterpret_cast<uint4*>(a->flags), n16, a->cnt, a->tick);
   return hipGetLastError();
 }
