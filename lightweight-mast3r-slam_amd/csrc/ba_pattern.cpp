@@ -103,22 +103,27 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P)
   P->sidx.clear();
   P->pull_grp.assign(nb, -1);
   std::vector<std::vector<int>> by_tgt(nb);  // j -> sources k of the current level
-  std::vector<int> touched, slot(nb, -1);
+  // slot[i] / stamp[i]: the block of the current source column k at row i, valid while stamp[i] == k + 1
+  std::vector<int> touched, slot(nb, -1), stamp(nb, 0);
   std::vector<int4_host> pull_groups;  // groups run inside factor tasks, appended after the step groups
+  P->src.reserve((size_t)4 * P->nL);
+  P->sidx.reserve((size_t)8 * P->nL);
   auto emit = [&](int j, const std::vector<int>& ks, std::vector<int4_host>& out) {
     const int s0 = (int)P->src.size() / 4;
     for (int k : ks) {
-      for (int q = P->col_ptr[k] + 1; q < P->col_ptr[k + 1]; q++) slot[P->rowL[q]] = q;
-      const int bjk = (int)(std::lower_bound(P->rowL.begin() + P->col_ptr[k] + 1, P->rowL.begin() + P->col_ptr[k + 1], j) -
-                            P->rowL.begin());
+      int bjk = -1;
+      for (int q = P->col_ptr[k] + 1; q < P->col_ptr[k + 1]; q++) {
+        slot[P->rowL[q]] = q;
+        stamp[P->rowL[q]] = k + 1;
+        if (P->rowL[q] == j) bjk = q;
+      }
       P->src.push_back(bjk);
       P->src.push_back(k);
       P->src.push_back((int)P->sidx.size());
       P->src.push_back(0);
       for (int b = P->col_ptr[j]; b < P->col_ptr[j + 1]; b++) {
         const int i = P->rowL[b];
-        const bool in = std::binary_search(P->rowL.begin() + P->col_ptr[k] + 1, P->rowL.begin() + P->col_ptr[k + 1], i);
-        P->sidx.push_back(in ? slot[i] : -1);
+        P->sidx.push_back(stamp[i] == k + 1 ? slot[i] : -1);
       }
     }
     out.push_back(make_int4_host(j, s0, (int)P->src.size() / 4));

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_tracking.py tests/test_gpu_configs.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/track_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_matching.py tests/test_gpu_tracking.py tests/test_gpu_configs.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/track_tests.log 2>&1
 rc=$?; echo "TRACK_TESTS_RC=$rc"; tail -3 gpurun_out/track_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu --no-ba --no-peaks --no-retrieval > gpurun_out/bench_track.json 2> gpurun_out/bench_track.err
 rc=$?; echo "BENCH_RC=$rc"; [ $rc -eq 0 ] || exit $rc
