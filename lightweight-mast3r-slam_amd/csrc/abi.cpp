@@ -683,20 +683,39 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     if (!strcmp(f, "sparse")) P.dense = 0;
     if (!strcmp(f, "dense") && P.a.H) P.dense = 1;
   }
-  // factor steps wider than one workgroup's 16 waves run as multi-workgroup launches: every step up to the
-  // last such step (the leaf end of the elimination tree; measured: ~12 rounds of 16 waves per leaf step in
-  // one workgroup), the narrow root end stays in the one-workgroup kernel
+  // the leaf end of the elimination tree runs as multi-workgroup launches (steps [0, wide_steps)), the root end
+  // in the one-workgroup kernel. The split minimises the measured step costs (MI355X, C5/C4 graphs): a launch
+  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of 16 waves (one wave per task).
+  // M3S_BA_WIDE=t (tests, experiments): every step up to the last one with more than t tasks instead.
   {
-    int thr = 16;
-    if (const char* w = getenv("M3S_BA_WIDE")) thr = atoi(w);  // experiments: 0 = every step, huge = none
-    int last = -1;
+    std::vector<int> tasks(S.nlev + 1);
     for (int l = 0; l <= S.nlev; l++) {
       const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
-      const int tasks = na + S.grp_ptr[l + 1] - S.grp_ptr[l];
-      if (l < BA_MAX_WIDE_STEPS) P.step_tasks[l] = tasks;
-      if (tasks > thr) last = l;
+      tasks[l] = na + S.grp_ptr[l + 1] - S.grp_ptr[l];
+      if (l < BA_MAX_WIDE_STEPS) P.step_tasks[l] = tasks[l];
     }
-    P.a.wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+    const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
+    if (const char* w = getenv("M3S_BA_WIDE")) {
+      const int thr = atoi(w);
+      int last = -1;
+      for (int l = 0; l <= S.nlev; l++)
+        if (tasks[l] > thr) last = l;
+      P.a.wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+    } else {
+      constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
+      std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
+      for (int l = lmax - 1; l >= 0; l--) suffix[l] = suffix[l + 1] + kRoundUs * ((tasks[l] + 15) / 16);
+      int best_L = 0;
+      double best = suffix[0];
+      for (int L = 1; L <= lmax; L++) {
+        const double c = kLaunchUs * L + suffix[L];
+        if (c < best) {
+          best = c;
+          best_L = L;
+        }
+      }
+      P.a.wide_steps = best_L;
+    }
   }
   P.a.bad = P.a.info + 3;
   P.a.plan_lo = reinterpret_cast<const char*>(P.a.col_ptr);
