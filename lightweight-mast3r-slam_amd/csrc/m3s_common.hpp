@@ -12,13 +12,6 @@
 
 namespace m3s {
 
-__device__ __forceinline__ float huber_ba(float r) {  // gn_kernels.cu:172-175, k = 1.345 (double)
-  const float r_abs = fabsf(r);
-  // r_abs < 1.345 (double compare) == r_abs < 1.345f for every float r_abs; the quotient is a
-  // double division rounded to float, evaluated only on the (rare) outlier branch.
-  return r_abs < 1.345f ? 1.0f : (float)(1.345 / (double)r_abs);
-}
-
 __device__ __forceinline__ void quat_comp(const float* qi, const float* qj, float* out) {
   out[0] = qi[3] * qj[0] + qi[0] * qj[3] + qi[1] * qj[2] - qi[2] * qj[1];
   out[1] = qi[3] * qj[1] - qi[0] * qj[2] + qi[1] * qj[3] + qi[2] * qj[0];
