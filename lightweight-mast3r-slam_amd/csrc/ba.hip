@@ -99,9 +99,46 @@ __device__ __forceinline__ void actSO3_v(const float* q, const f2* X, f2* Y) {
   Y[2] = X[2] + q[3] * uv2 + (q[0] * uv1 - q[1] * uv0);
 }
 
+// BA_PAIR_ACC: the fp64 accumulators are split between the two lanes of a lane pair (even lane: sums 0..17,
+// odd lane: 18..34), 18 doubles per lane instead of 35, which brings the kernel under the 3-waves-per-SIMD
+// VGPR budget. At each flush a lane hands the partner the run sums the partner owns (DPP swaps) and adds its
+// own and the partner's fp32 run sums of both points in fp64: the same BA_RUN_LEN-point fp32 runs as with
+// per-lane accumulators (folding a lane's two points in fp32 first took the 6-KF rays fixture to 1.6e-5
+// from the fp64 truth, over the 1e-5 contract).
+#ifndef BA_PAIR_ACC
+#define BA_PAIR_ACC 1
+#endif
 #ifndef BA_LIN_WAVES  // waves per SIMD the linearisation is compiled for (VGPR budget 512 / waves)
+#if BA_PAIR_ACC
+#define BA_LIN_WAVES 3
+#else
 #define BA_LIN_WAVES 2
 #endif
+#endif
+#define BA_PAIR_HALF 18  // sums owned per lane of a pair (35 = 18 + 17)
+
+__device__ __forceinline__ float dpp_swap1(float x) {  // quad_perm [1,0,3,2]: the value of lane ^ 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+
+// each lane of the pair (lane ^ 1) adds the fp32 run sums (28 L + 7 v, both points) of the sums it owns, its
+// own and the partner's, into its fp64 accumulators
+__device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* fv, bool odd) {
+  const f2 z2 = {0.0f, 0.0f};
+#pragma unroll
+  for (int m = 0; m < BA_PAIR_HALF; m++) {
+    const f2 lo = m < 28 ? fL[m] : fv[m - 28];
+    const int c = BA_PAIR_HALF + m;
+    const f2 hi = c < 28 ? fL[c] : (c < 35 ? fv[c - 28] : z2);
+    const f2 own = odd ? hi : lo;
+    const f2 give = odd ? lo : hi;  // the partner owns the other half
+    const f2 got = {dpp_swap1(give.x), dpp_swap1(give.y)};
+    acc[m] += (double)own.x;
+    acc[m] += (double)own.y;
+    acc[m] += (double)got.x;
+    acc[m] += (double)got.y;
+  }
+}
 
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
 //   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
@@ -152,11 +189,18 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     Tj[c] = a.Twc[jx * 8 + c];
   }
   relSim3(Ti, Tj, Tij);
+#if BA_PAIR_ACC
+  const bool odd = threadIdx.x & 1;
+  double acc[BA_PAIR_HALF];
+#pragma unroll
+  for (int m = 0; m < BA_PAIR_HALF; m++) acc[m] = 0.0;
+#else
   double L[28], v[7];
 #pragma unroll
   for (int c = 0; c < 28; c++) L[c] = 0.0;
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
+#endif
   const float4* rec = a.rec + (size_t)e * N;
   const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
@@ -170,7 +214,11 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
   int run = 0;
   // two points per lane per round, (k0, k0 + blockDim): every per-point float operation runs on both at once
   // as one packed fp32 instruction (v_pk_fma/mul/add_f32; float2 lanes), the transcendentals per component
-  for (int k0 = k_begin + threadIdx.x; k0 < k_end; k0 += 2 * blockDim.x) {
+  // a block-uniform trip count: every lane reaches each run flush together (the pair flush swaps run sums
+  // between the lanes of a pair); a lane past the chunk's end skips the point work
+  for (int k00 = k_begin; k00 < k_end; k00 += 2 * blockDim.x) {
+    const int k0 = k00 + (int)threadIdx.x;
+    if (k0 < k_end) {
     const int k1 = k0 + (int)blockDim.x;
     const bool has1 = k1 < k_end;
     // a missing second point repeats the first with weight 0: it adds exact zeros unless the first point's own
@@ -251,8 +299,16 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b0111110>(fL, fv, J1, huber_ba2(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
       acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
+    }
     if (++run == BA_RUN_LEN) {  // the run's fp32 sums (BA_RUN_LEN points per slot) into the fp64 accumulators
       run = 0;
+#if BA_PAIR_ACC
+      pair_flush(acc, fL, fv, odd);
+#pragma unroll
+      for (int c = 0; c < 28; c++) fL[c] = f2{0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < 7; c++) fv[c] = f2{0.0f, 0.0f};
+#else
 #pragma unroll
       for (int c = 0; c < 28; c++) {
         L[c] += (double)fL[c].x;
@@ -265,8 +321,23 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
         v[c] += (double)fv[c].y;
         fv[c] = f2{0.0f, 0.0f};
       }
+#endif
     }
   }
+  __shared__ double s_part[4][BA_NSUM];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#if BA_PAIR_ACC
+  pair_flush(acc, fL, fv, odd);
+  // butterfly over the lanes of one parity (offsets 32..2), then 4 waves through LDS
+#pragma unroll
+  for (int m = 0; m < BA_PAIR_HALF; m++) {
+    double t = acc[m];
+#pragma unroll
+    for (int off = 32; off > 1; off >>= 1) t += __shfl_xor(t, off, 64);
+    const int c = odd ? BA_PAIR_HALF + m : m;
+    if (lane < 2 && c < 35) s_part[wid][c] = t;
+  }
+#else
 #pragma unroll
   for (int c = 0; c < 28; c++) {
     L[c] += (double)fL[c].x;
@@ -278,8 +349,6 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     v[c] += (double)fv[c].y;
   }
   // wave64 butterfly in fp64, then 4 waves through LDS
-  __shared__ double s_part[4][BA_NSUM];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < 28; c++) {
     const double t = wave_sum(L[c]);
@@ -290,6 +359,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     const double t = wave_sum(v[c]);
     if (lane == 0) s_part[wid][28 + c] = t;
   }
+#endif
   __syncthreads();
   if (threadIdx.x < 35) {
     const int c = threadIdx.x;
