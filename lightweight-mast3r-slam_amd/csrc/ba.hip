@@ -39,8 +39,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // them; ~45% of the FMAs in rays mode). Products and sums in fp32 (packed: two points per instruction) over
 // runs of BA_RUN_LEN rounds per slot, each run then added to the fp64 accumulators (the kernel is VALU-issue
 // bound; fp64 products put no measurable accuracy gain against the fp64 truth once runs are short).
-#ifndef BA_RUN_LEN  // rounds per fp32 run: 8 points per slot (4: 2.40 -> 8: 2.30 ms at C5, both within 1e-5 of the truth)
-#define BA_RUN_LEN 8
+#ifndef BA_RUN_LEN  // rounds per fp32 run (points per slot): 8 -> 16 took C5 2.25 -> 2.19 ms, C4 1.91 -> 1.83 ms;
+#define BA_RUN_LEN 16  // the 48-round full-chunk graphs stay within 1e-5 of the fp64 truth
 #endif
 template <unsigned MASK>
 __device__ __forceinline__ void acc_local_f2(f2* L, f2* v, const f2 J[7], f2 w, f2 e) {

@@ -259,6 +259,31 @@ def test_ba_medium_graph_vs_fp64_truth(mode):
     np.testing.assert_allclose(T, T_ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_ba_full_chunk_runs_vs_fp64_truth(mode):
+    """6 keyframes at 128x192 = 24576 points per edge, one full linearisation chunk: every lane walks 48 point
+    rounds, so the fp32 runs are flushed into the fp64 accumulators several times (the smaller graphs end
+    inside the first run). Poses within 1e-5 of the oracle's fp64 truth."""
+    from m3s.synthetic import make_graph, two_way
+
+    H, W = 128, 192
+    G = make_graph(n_kf=6, H=H, W=W, seed=11)
+    ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
+    K = G["K"].numpy()
+    Xs = G["Xs"].numpy()
+    if mode == "calib":
+        Xs = O.backproject_constrain(Xs, K, (H, W))
+    Cs = G["Cs"].numpy()
+    sa, sb = SIG[mode]
+    p = O.ba_params(mode, sa, sb, 0.0, 1.5, K=K, height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    T_ref, _, _ = O.gauss_newton_f64(mode, G["Twc0"].numpy().astype(np.float64), Xs.astype(np.float64),
+                                     Cs[..., 0].astype(np.float64), ii, jj, idx, valid[..., 0],
+                                     Q[..., 0].astype(np.float64), p, 10, 1e-8)
+    T, dx = _call(mode, G["Twc0"].numpy(), Xs, Cs, ii, jj, idx, valid, Q, K, H, W)
+    assert np.isfinite(T).all()
+    np.testing.assert_allclose(T, T_ref, atol=1e-5)
+
+
 @pytest.mark.gpu
 def test_zero_copy_keyframe_plan_equals_stacked(golden):
     """m3s_ba_make_plan_kf (keyframes' own X_canon / C-sum buffers) == the stacked plan
