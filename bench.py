@@ -166,23 +166,45 @@ KERNEL_SYMBOL = {"prep_rays": "prep_rays_kernel", "proj_occlusion": "proj_occlus
                  "refine_lin": "refine_tile_kernel", "track_setup": "track_setup_kernel", "gn_iters": "gn_loop_kernel"}
 
 
-def pmc_traffic(name, pattern="r[0-9][0-9]_pmc.json"):
-    """HBM bytes per launch of `name` from the newest committed rocprofv3 PMC summary
-    (profiles/<round>_pmc.json, FETCH_SIZE x2 + WRITE_SIZE, scripts/profile_summary.py); None if absent."""
+def pmc_entry(name, pattern="r[0-9][0-9]_pmc.json"):
+    """The newest committed rocprofv3 PMC summary entry of kernel `name` (profiles/<round>_*pmc.json,
+    FETCH_SIZE x2 + WRITE_SIZE per launch, scripts/profile_summary.py) with its file name; None if absent."""
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", pattern)))
     if not files:
         return None
     for k, v in json.load(open(files[-1])).items():
         if KERNEL_SYMBOL.get(name, name) in k:
-            return v["traffic_bytes"]
+            return dict(v, file=os.path.basename(files[-1]))
     return None
+
+
+def pmc_traffic(name, pattern="r[0-9][0-9]_pmc.json"):
+    e = pmc_entry(name, pattern)
+    return e["traffic_bytes"] if e else None
 
 
 # SURVEY.md §8(d) BA legs: C5 = 256-keyframe chess graph, calib, 512x384 (7-Scenes shape); C4 = EuRoC-shaped
 # graph (MH_02_easy trajectory), rays (eval_no_calib), 512x320
 BA_LEGS = {"C5": dict(traj="chess", mode="calib", H=384, W=512), "C4": dict(traj="euroc", mode="rays", H=320, W=512)}
-BA_BYTES_PER_POINT = 45  # SURVEY.md §8(d): Xi gather 12 + idx 8 + valid 1 + Xj 12 + Q 4 + Ci 4 + Cj 4
-BA_BYTES_PER_EDGE = 840  # Hs / gs out
+# Compulsory HBM bytes of the build's BA loop (DESIGN.md §4). Once per call the pack streams, per point and edge,
+# valid 1 + idx 8 + Q 4 in and the 16-B record out (29 B), and gathers from the keyframes' X (12 B) and C (4 B),
+# compulsory once per keyframe point. Every GN iteration then streams only the 16-B record of each point of each
+# edge and the 12-B X_j of each point of each distinct target keyframe (the edges of one target share that slab in
+# L2), plus per edge its chunk partials (36 doubles written by ba_lin, read back by ba_edge) and its edge-sum row.
+BA_PACK_EDGE_BYTES = 29
+BA_PACK_KF_BYTES = 16
+BA_REC_BYTES = 16
+BA_XJ_BYTES = 12
+BA_SUM_BYTES = 36 * 8
+
+
+def ba_plan_info(lib, plan):
+    from m3s import _lib
+
+    info = (ctypes.c_int * 8)()
+    _lib.check(lib.m3s_ba_plan_info(ctypes.byref(plan), info))
+    keys = ("chunks", "factor_blocks", "levels", "wide_steps", "dense", "targets", "edges", "poses")
+    return dict(zip(keys, list(info)))
 
 
 def bench_ba(args, rank, world, dev, leg):
@@ -201,16 +223,18 @@ def bench_ba(args, rank, world, dev, leg):
     Xs, Cs = G["Xs"].contiguous(), G["Cs"][..., 0].contiguous()
     if mode == "calib":  # global_opt.py:163-201: the calib solve sees the points constrained to their rays
         Xs = constrain_points_to_ray((H, W), Xs, G["K"]).contiguous()
+    Twc0 = G["Twc0"].clone()  # the stated initial poses; every call starts from a fresh copy
     E = ii.shape[0]
     N = H * W
     e0, e1 = shard_range(E, rank, world)
     cfg = ba_config(mode, config["local_opt"], K=G["K"], height=H, width=W)
     lib = _lib.load()
+    names = ("ba_pack", "ba_linearize", "ba_solve")
 
     def run(iters, timed_kernels=False):
         # the whole gauss_newton call is timed: plan (rank remap, symbolic factorisation, per-call
         # point records of this rank's edges) + iters x (linearise, all-reduce, solve, retract)
-        Twc = G["Twc0"].to(dev).contiguous()
+        Twc = Twc0.clone()  # gauss_newton mutates Twc in place (gn.cpp): never the graph's own initial poses
         sync_all(world)
         if timed_kernels:
             lib.m3s_timing_reset()
@@ -225,35 +249,50 @@ def bench_ba(args, rank, world, dev, leg):
         spans = {}
         if timed_kernels:
             lib.m3s_timing_enable(0)
-            for name in ("ba_linearize", "ba_solve"):
+            for name in names:
                 ms, cnt = ctypes.c_double(), ctypes.c_int()
                 _lib.check(lib.m3s_timing_query(name.encode(), ms, cnt))
                 spans[name] = ms.value / max(cnt.value, 1)
-        return el, t1 - t0, spans
+        return el, t1 - t0, spans, shard, Twc
 
     run(1)  # warmup
-    el, setup, _ = run(args.ba_iters)
+    el, setup, _, shard, Twc = run(args.ba_iters)
     el = max_over_ranks(el, world)
     setup = max_over_ranks(setup, world)
-    _, _, spans = run(args.ba_iters, timed_kernels=True)  # HIP-event spans, a second pass (events cost host time)
-    st = _lib.ba_pattern_stats(ii.cpu().numpy(), jj.cpu().numpy(), args.ba_kf)
-    # roofline of the dominant kernel (the linearisation) at SURVEY §8(d)'s algorithmic bytes per edge-iteration
+    _, _, spans, _, Twc2 = run(args.ba_iters, timed_kernels=True)  # HIP-event spans, a second pass
+    assert torch.equal(Twc, Twc2), "BA: two calls from the same initial poses differ"
+    info = ba_plan_info(lib, shard.plan)
+    # roofline of the dominant kernel (the linearisation) at the build's compulsory bytes per iteration
     lin_s = spans["ba_linearize"] * 1e-3
-    alg = (e1 - e0) * (BA_BYTES_PER_POINT * N + BA_BYTES_PER_EDGE)
-    traffic = pmc_traffic("ba_lin_kernel", pattern="r[0-9][0-9]_ba_pmc.json")
+    n_e = e1 - e0
+    alg = n_e * N * BA_REC_BYTES + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
+    pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}>",
+                    pattern=f"r[0-9][0-9]_ba{'_c4' if leg == 'C4' else ''}_pmc.json")
+    traffic = pmc["traffic_bytes"] if pmc else None
     roof = {"kernel": "ba_lin_kernel + ba_edge_kernel", "bound": "hbm", "achieved": alg / lin_s / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / lin_s / 1e9 / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_over_alg": (traffic / alg) if traffic else None,
-            "avg_us": spans["ba_linearize"] * 1e3,
-            "alg_bytes": f"{BA_BYTES_PER_POINT} B/point x {N} points + {BA_BYTES_PER_EDGE} B per edge-iteration "
-                         f"(SURVEY.md 8d), x {e1 - e0} edges per launch"}
+            "traffic_source": pmc["file"] if pmc else None, "avg_us": spans["ba_linearize"] * 1e3,
+            "alg_bytes": f"{BA_REC_BYTES} B record x {N} points x {n_e} edges + {BA_XJ_BYTES} B X_j x {N} points x "
+                         f"{info['targets']} target keyframes + {2 * info['chunks'] + 1} x {BA_SUM_BYTES} B partial/"
+                         f"edge-sum rows x {n_e} edges per launch (compulsory traffic, DESIGN.md §4)"}
+    pack_s = spans["ba_pack"] * 1e-3
+    pack_bytes = n_e * N * BA_PACK_EDGE_BYTES + args.ba_kf * N * BA_PACK_KF_BYTES
+    pack_pmc = pmc_entry(f"ba_pack_kernel<{1 if mode == 'rays' else 2}>",
+                         pattern=f"r[0-9][0-9]_ba{'_c4' if leg == 'C4' else ''}_pmc.json")
     out = {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
            "points_per_kf": N, "shape": [H, W], "mode": mode, "trajectory": L["traj"], "iters": args.ba_iters,
            "ms_per_call": el * 1e3, "ms_setup": setup * 1e3, "ms_per_iter": (el - setup) / args.ba_iters * 1e3,
+           "ms_pack": spans["ba_pack"], "ms_plan_host": max(setup * 1e3 - spans["ba_pack"], 0.0),
            "ms_lin_per_iter": spans["ba_linearize"], "ms_solve_per_iter": spans["ba_solve"],
-           "factor": {"blocks": st[0], "levels": st[1], "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2},
-           "scaling": "strong", "roofline": roof}
-    del G, idx, valid, Q, Xs, Cs
+           "factor": {"blocks": info["factor_blocks"], "levels": info["levels"], "wide_steps": info["wide_steps"],
+                      "dense": bool(info["dense"]), "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2},
+           "scaling": "strong", "roofline": roof,
+           "pack": {"GBps": pack_bytes / pack_s / 1e9, "frac": pack_bytes / pack_s / 1e9 / HBM_PEAK_GBS,
+                    "bytes": pack_bytes, "traffic": pack_pmc["traffic_bytes"] if pack_pmc else None,
+                    "note": f"once per call: {BA_PACK_EDGE_BYTES} B per point and edge + {BA_PACK_KF_BYTES} B per "
+                            f"keyframe point (compulsory)"}}
+    del G, idx, valid, Q, Xs, Cs, shard
     torch.cuda.empty_cache()
     return out
 
@@ -278,18 +317,24 @@ def ba_cpu_baseline(args, leg="C5", n_kf=8, iters=2):
                     z_eps=c["depth_eps"])
     E = G["ii"].shape[0]
     out = {}
-    for label, threads, its in (("all_cores", min(16, len(os.sched_getaffinity(0))), iters), ("one_thread", 1, 1)):
+    avail = len(os.sched_getaffinity(0))
+    legs = [("all_cores", avail, iters), ("one_thread", 1, 1)]
+    if avail > 16:
+        legs.insert(1, ("box_share", 16, iters))
+    for label, threads, its in legs:
         O.set_threads(threads)
         t0 = time.perf_counter()
         O.gauss_newton(mode, G["Twc0"].numpy(), Xs, G["Cs"].numpy()[..., 0], G["ii"].numpy(), G["jj"].numpy(),
                        G["idx"].numpy(), G["valid"].numpy()[..., 0], G["Q"].numpy()[..., 0], p, its, 0.0)
         el = time.perf_counter() - t0
         out[label] = {"value": E * its / el, "cores": threads, "seconds": el}
-    O.set_threads(min(16, len(os.sched_getaffinity(0))))
+    O.set_threads(min(16, avail))
+    share = out.get("box_share")
     return {"value": out["all_cores"]["value"], "unit": "edges/s", "cores": out["all_cores"]["cores"], "kind": "port",
-            "one_thread": out["one_thread"]["value"],
+            "one_thread": out["one_thread"]["value"], "affinity_cores": avail,
+            "box_share_16": share["value"] if share else None,
             "sample": f"{leg} shape ({H}x{W}, {mode}), first {n_kf} keyframes ({E} directed edges) through the oracle's "
-                      f"gauss_newton (C, OpenMP): {iters} iterations on all cores in {out['all_cores']['seconds']:.1f}s, "
+                      f"gauss_newton (C, OpenMP): {iters} iterations on all {avail} cores in {out['all_cores']['seconds']:.1f}s, "
                       f"1 on one thread in {out['one_thread']['seconds']:.1f}s"}
 
 
@@ -411,12 +456,11 @@ def cpu_model():
 
 def cpu_baseline(args):
     """Oracle (C restatement + numpy glue) on the host cores, bounded sample of the same workload: frames on
-    all cores (up to 16, the box's share) for ~cpu_seconds, then one frame on one thread."""
+    every core of the affinity mask for ~cpu_seconds, on the box's 16-core share, then one frame on one thread."""
     import oracle.oracle as O
     from m3s.synthetic import make_pair
 
     avail = len(os.sched_getaffinity(0))
-    cores = min(16, avail)
     H, W = args.height, args.width
     P = make_pair(H, W, seed=0)
     X, C, D, Q = (P[k].numpy() for k in ("X", "C", "D", "Q"))
@@ -438,24 +482,31 @@ def cpu_baseline(args):
         else:
             O.track_rays(X[0].reshape(-1, 3)[i], Xk, I, I, Qk, v)
 
-    O.set_threads(cores)
-    t0 = time.perf_counter()
-    frames = 0
-    while True:
-        frame()
-        frames += 1
-        if time.perf_counter() - t0 > args.cpu_seconds or frames >= 50:
-            break
-    el = time.perf_counter() - t0
+    def timed(threads, seconds):
+        O.set_threads(threads)
+        t0 = time.perf_counter()
+        frames = 0
+        while True:
+            frame()
+            frames += 1
+            if time.perf_counter() - t0 > seconds or frames >= 50:
+                break
+        return frames, time.perf_counter() - t0
+
+    frames, el = timed(avail, args.cpu_seconds)  # every host core this process may run on
+    share = timed(16, args.cpu_seconds / 2) if avail > 16 else None  # the box's CPU share (16 per GPU)
     O.set_threads(1)
     t1 = time.perf_counter()
     frame()
     el1 = time.perf_counter() - t1
-    O.set_threads(cores)
-    return {"value": frames / el, "unit": "tracked frames/s", "cores": cores, "kind": "port",
+    O.set_threads(min(16, avail))
+    return {"value": frames / el, "unit": "tracked frames/s", "cores": avail, "kind": "port",
             "one_thread": 1.0 / el1, "affinity_cores": avail, "cpu_model": cpu_model(),
-            "sample": f"{frames} tracked frames ({H}x{W}, {args.mode}) through oracle/ (C kernels, OpenMP {cores} "
-                      f"threads, + numpy fp64 glue) in {el:.1f}s; one frame on one thread in {el1:.1f}s"}
+            "box_share_16": share[0] / share[1] if share else None,
+            "sample": f"{frames} tracked frames ({H}x{W}, {args.mode}) through oracle/ (C kernels, OpenMP {avail} "
+                      f"threads = len(sched_getaffinity), + numpy fp64 glue) in {el:.1f}s"
+                      + (f"; {share[0]} frames on 16 threads in {share[1]:.1f}s" if share else "")
+                      + f"; one frame on one thread in {el1:.1f}s"}
 
 
 def main():

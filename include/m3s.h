@@ -77,6 +77,9 @@ typedef struct m3s_ba_config {
   float z_eps;
 } m3s_ba_config;
 
+/* Kp <= M3S_BA_MAX_POSES: the workspace is sized for the densest factor pattern of Kp poses (no edges are known
+ * to the size query): nb (nb + 1) / 2 blocks of 512 B for nb = Kp - 1, 4.3 GB at the cap. */
+#define M3S_BA_MAX_POSES 4096
 size_t m3s_ba_workspace_size(int Kp, int N, int E);
 int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
                      const int64_t* ii, const int64_t* jj, int E, const int64_t* idx, const uint8_t* valid,
@@ -110,6 +113,11 @@ int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /* syncs the stream */
+/* Host-only facts of a built plan (bench rooflines, tests): info[0] = linearisation chunks per edge,
+ * [1] = factor blocks, [2] = elimination-tree levels, [3] = multi-workgroup factor steps, [4] = 1 if the dense
+ * fallback factorisation is used, [5] = distinct target keyframes among the shard's edges, [6] = shard edges,
+ * [7] = poses. */
+int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info);
 /* Host-only diagnostic of the symbolic factorisation the plan builds for these edges (host arrays):
  * stats[0] = factor blocks (7x7, diagonal included), [1] = elimination-tree levels, [2] = update groups
  * (source level, target column), [3] = update sources, [4] = source-map entries, [5] = groups run by
@@ -136,6 +144,10 @@ int m3s_match(const float* X11, const float* X21, const float* D11, const float*
 #define M3S_TRACK_MAX_ITERS 2
 #define M3S_TRACK_CHOLESKY_FAILED 3
 #define M3S_TRACK_SKIPPED 4
+/* The persistent GN launch's blocks did not all become resident within the bounded spin (e.g. the GPU
+ * was shared with long-running persistent work): m3s_track then returns M3S_EHIP ("hand-off stalled")
+ * instead of a result, never a silent relocalisation. */
+#define M3S_TRACK_STALLED 5
 
 typedef struct m3s_track_config {
   int mode;           /* 0 rays (use_calib False), 1 calib */

@@ -33,6 +33,7 @@ hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStrea
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
 hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, const TrackPublish*, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
+int m3s_track_max_parts(void);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, hipStream_t);
@@ -410,7 +411,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
   }
   (void)first_chunk;  // every GN iteration runs inside one persistent launch (gn_loop_kernel)
-  const int nparts = track_nparts(N);
+  const int nparts = std::min(track_nparts(N), m3s_track_max_parts());  // every block co-resident
   TrackMirror* mirror = pinned_mirror();
   if (mirror == nullptr) return fail(M3S_EHIP, "track: pinned result mirror allocation failed");
   static thread_local unsigned gen = 0;
@@ -426,6 +427,9 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   HIP_TRY(m3s_launch_fuse(&a, 0, &fa, p.direct ? 0 : 1, N, &pub, s), "track fuse launch");
   if (int rc = wait_published(mirror, pub.gen, s)) return rc;
   const TrackState& hs = mirror->s;
+  if (hs.status == M3S_TRACK_STALLED)
+    return fail(M3S_EHIP, "track: the persistent GN launch's hand-off stalled (its blocks were not co-resident); "
+                          "no pose for this frame");
   memcpy(result->T_WCf, hs.T_WCf, sizeof(result->T_WCf));
   memcpy(result->T_CkCf, hs.T, sizeof(result->T_CkCf));
   result->cost = hs.last_cost;
@@ -452,6 +456,7 @@ struct BaPlanImpl {
   int nL;
   int step_tasks[BA_MAX_WIDE_STEPS];  // tasks (waves) of each multi-workgroup factor step
   int dense;  // 1: the dense fallback factorisation (ba_dense.hip)
+  int n_targets;  // distinct target keyframes j among this shard's edges (their X_j slabs are streamed per iteration)
   float delta_thresh;
   size_t edge_sums_off, edge_sums_bytes;
   void* ws;
@@ -459,11 +464,21 @@ struct BaPlanImpl {
 static_assert(sizeof(BaPlanImpl) <= sizeof(m3s_ba_plan), "m3s_ba_plan too small");
 
 // points of one keyframe per linearisation block: 24576 x 12 B = 295 KB of X_j, so the ~100 blocks an XCD
-// runs at once (the edges of a few target keyframes, same chunk) share their X_j slabs in its 4 MiB L2
-constexpr int BA_CHUNK_POINTS = 24576;
+// runs at once (the edges of a few target keyframes, same chunk) share their X_j slabs in its 4 MiB L2. Small
+// graphs (the early-sequence global optimisations) would leave most CUs idle at that length: their chunks
+// shrink (down to 4096 points, 8 rounds per lane) until E x chunks reaches 512 blocks. A function of the
+// FULL edge count, so every rank of a sharded solve cuts its edges exactly like the unsharded one.
+// M3S_BA_CHUNK_POINTS (tests): a fixed chunk length instead.
+constexpr int BA_CHUNK_POINTS = 24576, BA_CHUNK_MIN_POINTS = 4096, BA_LIN_MIN_BLOCKS = 512;
 int ba_chunks(int N, int E) {
-  (void)E;
-  return std::max(1, (N + BA_CHUNK_POINTS - 1) / BA_CHUNK_POINTS);
+  const int base = std::max(1, (N + BA_CHUNK_POINTS - 1) / BA_CHUNK_POINTS);
+  if (const char* f = getenv("M3S_BA_CHUNK_POINTS")) {
+    const int len = std::max(256, atoi(f));
+    return std::max(1, (N + len - 1) / len);
+  }
+  if ((int64_t)E * base >= BA_LIN_MIN_BLOCKS || E <= 0) return base;
+  const int most = std::max(1, (N + BA_CHUNK_MIN_POINTS - 1) / BA_CHUNK_MIN_POINTS);
+  return std::max(base, std::min(most, (BA_LIN_MIN_BLOCKS + E - 1) / E));
 }
 
 constexpr int BA_DENSE_MAX_POSES = 1025;  // dense fallback workspace: (2n+1) n doubles, ~0.8 GB at this size
@@ -520,9 +535,15 @@ struct PlanStage {
   hipEvent_t landed = nullptr;
   bool pending = false;
 };
+// one staging buffer + event per device: an event recorded on another device's stream would fail, and plans
+// for different GPUs need not serialise on one mutex
 PlanStage& plan_stage() {
-  static PlanStage st;
-  return st;
+  static std::mutex map_mu;
+  static std::map<int, PlanStage> stages;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(map_mu);
+  return stages[dev];  // std::map nodes never move
 }
 
 }  // namespace
@@ -548,7 +569,9 @@ extern "C" int m3s_ba_pattern_stats(const int64_t* ii, const int64_t* jj, int E,
     rj[e] = (int)(std::lower_bound(u.begin(), u.end(), jj[e]) - u.begin());
   }
   BaPattern P;
-  ba_build_pattern(ri.data(), rj.data(), E, Kp, &P);
+  M3S_CHECK(Kp <= M3S_BA_MAX_POSES, "ba pattern: at most 4096 poses (M3S_BA_MAX_POSES)");
+  ba_build_pattern(ri.data(), rj.data(), E, Kp, &P, ba_max_pairs(Kp));
+  if (P.too_dense) return fail(M3S_EINVAL, "ba pattern: too dense for the plan tables");
   stats[0] = P.nL;
   stats[1] = P.nlev;
   stats[2] = (int)P.grp.size() / 4;
@@ -568,7 +591,9 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
   M3S_CHECK(0 <= e0 && e0 <= e1 && e1 <= E, "ba: bad shard range");
-  M3S_CHECK(Kp <= 32768, "ba: at most 32768 poses");
+  // the workspace reserves the factor and plan tables of the densest pattern (m3s_ba_workspace_size knows no
+  // edges): nb(nb+1)/2 blocks of 512 B, 4.3 GB at this cap
+  M3S_CHECK(Kp <= M3S_BA_MAX_POSES, "ba: at most 4096 poses (M3S_BA_MAX_POSES)");
   if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
                                 "ba calib: height*width must equal the points per keyframe");
   if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");
@@ -599,7 +624,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   }
   // symbolic factorisation of the pose system (SparseBlock's pattern, gn_kernels.cu:71-113)
   BaPattern S;
-  ba_build_pattern(ri.data(), rj.data(), E, Kp, &S);
+  ba_build_pattern(ri.data(), rj.data(), E, Kp, &S, ba_max_pairs(Kp));
+  if (S.too_dense) return fail(M3S_EINVAL, "ba: factor pattern too dense for the plan tables");
   // linearisation block table: this shard's edges grouped by target keyframe j, chunk-major within a
   // group, so consecutive blocks (dealt to one XCD by xcd_remap) read the same X_j slab
   std::vector<int> lin_tab;
@@ -615,6 +641,10 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
         for (size_t t = g0; t < g1; t++) lin_tab.push_back(order[t] * chunks + c);
       g0 = g1;
     }
+  }
+  {
+    std::vector<char> seen(Kp, 0);
+    for (int e = e0; e < e1; e++) P.n_targets += seen[rj[e]] ? 0 : (seen[rj[e]] = 1);
   }
   // pack every table into one staging image of the device blob
   struct Sec {
@@ -754,7 +784,10 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.a.dx = dx_out ? dx_out : P.a.dx;
   // per-call point records of this shard's edges: the matched point, its pixel and the folded validity
   // weight do not change across GN iterations (only the poses do)
-  HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
+  {
+    Span sp("ba_pack", s);
+    HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
+  }
   memcpy(plan->opaque, &P, sizeof(P));
   return M3S_OK;
 }
@@ -795,6 +828,20 @@ extern "C" int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, si
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
   *byte_offset = P->edge_sums_off;
   *byte_count = P->edge_sums_bytes;
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
+  M3S_CHECK(plan && info, "ba: null argument");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  info[0] = P->p.chunks;
+  info[1] = P->nL;
+  info[2] = P->a.nlev;
+  info[3] = P->a.wide_steps;
+  info[4] = P->dense;
+  info[5] = P->n_targets;
+  info[6] = P->e1 - P->e0;
+  info[7] = P->Kp;
   return M3S_OK;
 }
 

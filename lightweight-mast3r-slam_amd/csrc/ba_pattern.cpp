@@ -3,6 +3,7 @@
 #include "ba_pattern.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 
 namespace {
@@ -20,7 +21,8 @@ inline int popcount_row(const uint64_t* r, int W) {
 
 }  // namespace
 
-void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P) {
+void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P, size_t max_sidx) {
+  max_sidx = std::min<size_t>(max_sidx, (size_t)INT32_MAX / 2);
   const int nb = std::max(0, Kp - 1);
   P->nb = nb;
   const int W = (nb + 63) / 64;
@@ -130,6 +132,10 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P)
   };
   std::vector<int4_host> step_groups;
   for (int l = 0; l < nlev; l++) {  // sources at level l
+    if (P->sidx.size() > max_sidx) {  // too dense for the plan tables: stop before host memory runs out
+      P->too_dense = true;
+      return;
+    }
     touched.clear();
     for (int c = P->lev_ptr[l]; c < P->lev_ptr[l + 1]; c++) {
       const int k = P->lev_col[c];

@@ -16,12 +16,14 @@
 //   * the assembly CSR in factor-block order: the contributions (edge*2 + sign) of each block, in edge
 //     order, and the rhs contributions per (new) block row.
 #pragma once
+#include <cstddef>
 #include <vector>
 
 struct BaPattern {
   int nb = 0;    // block columns (poses without the pinned one)
   int nL = 0;    // factor blocks (diagonal included)
   int nlev = 0;  // elimination-tree levels
+  bool too_dense = false;  // the update source map outgrew max_sidx: the build stopped early (tables incomplete)
   std::vector<int> perm;      // (nb) new column -> old (pin-removed) pose index
   std::vector<int> col_ptr;   // (nb+1) factor blocks of column j: [col_ptr[j], col_ptr[j+1]), first = diagonal
   std::vector<int> rowL;      // (nL) block row (new index) of each factor block
@@ -38,5 +40,7 @@ struct BaPattern {
   std::vector<int> rhs_ent;   // edge*2 + (1 if the row takes -g)
 };
 
-// ri, rj: dense pose ranks (pin 0 = rank 0 is fixed) of the E directed edges; Kp poses.
-void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P);
+// ri, rj: dense pose ranks (pin 0 = rank 0 is fixed) of the E directed edges; Kp poses. max_sidx bounds the
+// update source map (the plan's table capacity, < INT_MAX): past it the build stops with too_dense set, before a
+// dense large graph can exhaust host memory.
+void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P, size_t max_sidx = (size_t)1 << 30);

@@ -7,6 +7,7 @@
 #define M3S_TRACK_MAX_ITERS 2
 #define M3S_TRACK_CHOLESKY_FAILED 3
 #define M3S_TRACK_SKIPPED 4
+#define M3S_TRACK_STALLED 5  // the persistent GN launch lost a hand-off (blocks not co-resident): an error, not a result
 
 #define M3S_TRACK_SHARDS 8  // counter shards (one per XCD: blocks are dealt to XCDs round-robin)
 

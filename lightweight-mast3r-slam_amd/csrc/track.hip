@@ -399,8 +399,8 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
 // arrival ticket; the last arriver reduces the partials in a fixed order, solves, retracts, tests
 // convergence and broadcasts {T, cost, iter, done} through the GnBcast record; the other blocks poll
 // its generation word and continue with the new T (no kernel boundary, no empty launches after
-// convergence). Spins are bounded: a stalled hand-off ends the solve (status CHOLESKY_FAILED), never
-// hangs the GPU.
+// convergence). Spins are bounded: a stalled hand-off ends the solve (status STALLED, which the host reports
+// as an error), never hangs the GPU. The host sizes the grid by the occupancy query (m3s_track_max_parts).
 __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackParams p) {
   TrackState* st = a.state;
   if (st->done) return;
@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
         }
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 23)) {  // a lost hand-off: stop (status CHOLESKY_FAILED, dx of this frame dropped)
+        if (++spins > (1u << 23)) {  // a lost hand-off (~0.25 s): stop with status STALLED (the host raises)
           if (threadIdx.x == 0) s_stop = 1;
           break;
         }
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     __syncthreads();
     if (s_stop) {
       if (threadIdx.x == 0) {
-        wt(&st->status, M3S_TRACK_CHOLESKY_FAILED);
+        wt(&st->status, M3S_TRACK_STALLED);
         wt(&st->done, 1);
       }
       return;
@@ -688,6 +688,24 @@ extern "C" hipError_t m3s_launch_track_init(const TrackArgs* a, const float* T_W
 extern "C" hipError_t m3s_launch_track_setup(const TrackArgs* a, const TrackParams* p, hipStream_t s) {
   hipLaunchKernelGGL(m3s::track_setup_kernel, dim3((p->N + 255) / 256), dim3(256), 0, s, *a, *p);
   return hipGetLastError();
+}
+
+// Blocks of gn_loop_kernel that can be resident at once on the current device (occupancy query x CUs,
+// cached per device): the persistent launch's grid never exceeds it, so on an otherwise idle GPU every block
+// is resident; work of other streams only delays blocks (finite kernels), and the bounded spin catches the rest.
+extern "C" int m3s_track_max_parts(void) {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1;
+  if (dev >= 0 && dev < 64 && cache[dev] > 0) return cache[dev];
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(m3s::gn_loop_kernel),
+                                                   GN_THREADS, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 1;
+  const int n = per_cu * cus > 1 ? per_cu * cus : 1;
+  if (dev >= 0 && dev < 64) cache[dev] = n;
+  return n;
 }
 
 // one persistent launch runs every GN iteration (iters and chunk_id are kept for the call sites)

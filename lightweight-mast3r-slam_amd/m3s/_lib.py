@@ -84,6 +84,7 @@ _SIGS = {
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_iterations": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), c_void_p], c_int),
+    "m3s_ba_plan_info": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int)], c_int),
     "m3s_ba_pattern_stats": ([c_void_p, c_void_p, c_int, c_int, ctypes.POINTER(c_int)], c_int),
     "m3s_peak_fma_f32": ([c_void_p, c_int, c_int, c_void_p], c_int),
     "m3s_match_workspace_size": ([c_int] * 4, c_size_t),

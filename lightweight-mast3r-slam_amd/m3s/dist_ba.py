@@ -105,11 +105,14 @@ class HipShard:
 
 
 def run_sharded(shard, max_iter, group=None):
-    """GN loop of one rank: linearise shard -> all-reduce edge sums -> identical solve/retract."""
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    """GN loop of one rank: linearise shard -> all-reduce edge sums -> identical solve/retract.
+
+    The all-reduce runs whenever a process group exists (also at world size 1, where it is the identity:
+    the RCCL path is then exercised on one GPU); without one the loop is the plain single-GPU solve."""
+    reduce = dist.is_available() and dist.is_initialized()
     for _ in range(int(max_iter)):
         shard.linearize()
-        if world > 1:
+        if reduce:
             dist.all_reduce(shard.edge_sums, op=dist.ReduceOp.SUM, group=group)
         shard.solve()
     return shard

@@ -44,7 +44,7 @@ E = ii.shape[0]
 cfg = ba_config(mode, config["local_opt"], K=G["K"], height=H, width=W)
 lib = _lib.load()
 for rep in range(2):
-    Twc = G["Twc0"].to(dev).contiguous()
+    Twc = G["Twc0"].to(dev).clone()  # gauss_newton mutates Twc in place: never the graph's own initial poses
     shard = HipShard(cfg, Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.0, 0, E)
     torch.cuda.synchronize()
     lib.m3s_timing_reset()

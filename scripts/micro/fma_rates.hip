@@ -1,62 +1,106 @@
-// VALU issue rates on gfx950 with several waves per SIMD: v_fma_f64 vs v_fma_f32 vs v_pk_fma_f32,
-// one block of T threads on one CU (T/256 waves per SIMD), 8 independent chains per lane.
+// VALU issue rates on gfx950 (MI355X) per instruction, at 1, 2 and 4 waves per SIMD: the measured constants
+// behind the issue floors in DESIGN.md §4 (refine: v_pk_mul_f16 / v_add_f16 / v_cvt_f16_f32 / v_pk_add_f16;
+// BA linearisation: v_pk_fma_f32 / v_fma_f32; the factorisation: v_fma_f64).
+//
+// One kernel per instruction: every lane runs `iters` x 8 independent instances (8 accumulators, inline asm so
+// the compiler can neither fold nor reorder them), timed by s_memtime (shader clock) between two barriers.
+// Grid: one block of T threads per CU on every CU (256 blocks), T = 256 / 512 / 1024 = 1 / 2 / 4 waves per SIMD.
+// cycles per wave-instruction per SIMD = dcycles / (waves_per_SIMD x iters x 8); the median block is printed.
+// build: hipcc --offload-arch=gfx950 -O3 -o fma_rates fma_rates.hip
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <cstdio>
-template <typename T>
-__global__ void k(T* out, unsigned long long* t, int iters) {
-  T acc[8];
-  for (int c = 0; c < 8; c++) acc[c] = (T)(c + threadIdx.x);
-  const T a = (T)1.0000001, b = (T)1e-7;
-  __syncthreads();
-  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (int i = 0; i < iters; i++)
-#pragma unroll
-    for (int c = 0; c < 8; c++) acc[c] = acc[c] * a + b;
-  __syncthreads();
-  unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  T s = 0;
-  for (int c = 0; c < 8; c++) s += acc[c];
-  out[threadIdx.x] = s;
-  if (threadIdx.x == 0) *t = t1 - t0;
-}
-typedef float f2 __attribute__((ext_vector_type(2)));
-__global__ void kp(float* out, unsigned long long* t, int iters) {
-  f2 acc[8];
-  for (int c = 0; c < 8; c++) acc[c] = f2{(float)c, (float)threadIdx.x};
-  const f2 a = {1.0000001f, 1.0000001f}, b = {1e-7f, 1e-7f};
-  __syncthreads();
-  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (int i = 0; i < iters; i++)
-#pragma unroll
-    for (int c = 0; c < 8; c++) acc[c] = __builtin_elementwise_fma(acc[c], a, b);
-  __syncthreads();
-  unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  float s = 0;
-  for (int c = 0; c < 8; c++) s += acc[c].x + acc[c].y;
-  out[threadIdx.x] = s;
-  if (threadIdx.x == 0) *t = t1 - t0;
-}
+#include <vector>
+
+#define BODY8(ASM)                          \
+  asm volatile(ASM : "+v"(r0) : "v"(k)); \
+  asm volatile(ASM : "+v"(r1) : "v"(k)); \
+  asm volatile(ASM : "+v"(r2) : "v"(k)); \
+  asm volatile(ASM : "+v"(r3) : "v"(k)); \
+  asm volatile(ASM : "+v"(r4) : "v"(k)); \
+  asm volatile(ASM : "+v"(r5) : "v"(k)); \
+  asm volatile(ASM : "+v"(r6) : "v"(k)); \
+  asm volatile(ASM : "+v"(r7) : "v"(k));
+
+#define KERNEL(NAME, T, ASM)                                                                          \
+  __global__ void NAME(T* out, unsigned long long* cyc, int iters) {                                  \
+    T r0 = (T)threadIdx.x, r1 = r0 + (T)1, r2 = r0 + (T)2, r3 = r0 + (T)3, r4 = r0 + (T)4, r5 = r0 + (T)5, \
+      r6 = r0 + (T)6, r7 = r0 + (T)7;                                                                 \
+    const T k = (T)1;                                                                                 \
+    __syncthreads();                                                                                  \
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();                                       \
+    for (int i = 0; i < iters; i++) {                                                                 \
+      BODY8(ASM)                                                                                      \
+    }                                                                                                 \
+    __syncthreads();                                                                                  \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();                                       \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;               \
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                                  \
+  }
+
+// 32-bit operand instructions (f16 / packed f16 / packed-f32 halves live in 32-bit VGPRs)
+KERNEL(k_fma_f32, float, "v_fma_f32 %0, %0, %1, %1")
+KERNEL(k_add_f32, float, "v_add_f32 %0, %0, %1")
+KERNEL(k_pk_mul_f16, unsigned, "v_pk_mul_f16 %0, %0, %1")
+KERNEL(k_pk_add_f16, unsigned, "v_pk_add_f16 %0, %0, %1")
+KERNEL(k_pk_fma_f16, unsigned, "v_pk_fma_f16 %0, %0, %1, %1")
+KERNEL(k_add_f16, unsigned, "v_add_f16 %0, %0, %1")
+KERNEL(k_mul_f16, unsigned, "v_mul_f16 %0, %0, %1")
+KERNEL(k_cvt_f16_f32, unsigned, "v_cvt_f16_f32 %0, %1")
+KERNEL(k_cvt_f32_f16, unsigned, "v_cvt_f32_f16 %0, %1")
+KERNEL(k_perm_b32, unsigned, "v_perm_b32 %0, %0, %1, %1")
+// 64-bit operands
+KERNEL(k_pk_fma_f32, double, "v_pk_fma_f32 %0, %0, %1, %1")
+KERNEL(k_pk_mul_f32, double, "v_pk_mul_f32 %0, %0, %1")
+KERNEL(k_fma_f64, double, "v_fma_f64 %0, %0, %1, %1")
+KERNEL(k_add_f64, double, "v_add_f64 %0, %0, %1")
+
+typedef void (*kfn)(void*, unsigned long long*, int);
+
 int main() {
-  void* o;
-  unsigned long long* t;
-  (void)hipMalloc(&o, 1024 * 8);
-  (void)hipMalloc(&t, 8);
-  const int it = 20000;
-  for (int T : {256, 512, 1024}) {
-    unsigned long long h;
-    hipLaunchKernelGGL(k<double>, dim3(1), dim3(T), 0, 0, (double*)o, t, it);
-    hipLaunchKernelGGL(k<double>, dim3(1), dim3(T), 0, 0, (double*)o, t, it);
-    (void)hipMemcpy(&h, t, 8, hipMemcpyDeviceToHost);
-    const double w = T / 256.0;  // waves per SIMD
-    printf("T=%4d (%.0f waves/SIMD) v_fma_f64: %.2f ns per wave-instr per SIMD", T, w, h * 10.0 / (it * 8.0 * w));
-    hipLaunchKernelGGL(k<float>, dim3(1), dim3(T), 0, 0, (float*)o, t, it);
-    hipLaunchKernelGGL(k<float>, dim3(1), dim3(T), 0, 0, (float*)o, t, it);
-    (void)hipMemcpy(&h, t, 8, hipMemcpyDeviceToHost);
-    printf(" | v_fma_f32: %.2f", h * 10.0 / (it * 8.0 * w));
-    hipLaunchKernelGGL(kp, dim3(1), dim3(T), 0, 0, (float*)o, t, it);
-    hipLaunchKernelGGL(kp, dim3(1), dim3(T), 0, 0, (float*)o, t, it);
-    (void)hipMemcpy(&h, t, 8, hipMemcpyDeviceToHost);
-    printf(" | v_pk_fma_f32: %.2f\n", h * 10.0 / (it * 8.0 * w));
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  const int blocks = cus;
+  void* out;
+  unsigned long long* cyc;
+  (void)hipMalloc(&out, (size_t)blocks * 1024 * 8);
+  (void)hipMalloc(&cyc, (size_t)blocks * 8);
+  struct K {
+    const char* name;
+    const void* fn;
+    int size;
+  };
+  const K ks[] = {
+      {"v_fma_f32", (const void*)k_fma_f32, 4},       {"v_add_f32", (const void*)k_add_f32, 4},
+      {"v_pk_fma_f32", (const void*)k_pk_fma_f32, 8}, {"v_pk_mul_f32", (const void*)k_pk_mul_f32, 8},
+      {"v_pk_mul_f16", (const void*)k_pk_mul_f16, 4}, {"v_pk_add_f16", (const void*)k_pk_add_f16, 4},
+      {"v_pk_fma_f16", (const void*)k_pk_fma_f16, 4}, {"v_add_f16", (const void*)k_add_f16, 4},
+      {"v_mul_f16", (const void*)k_mul_f16, 4},       {"v_cvt_f16_f32", (const void*)k_cvt_f16_f32, 4},
+      {"v_cvt_f32_f16", (const void*)k_cvt_f32_f16, 4}, {"v_perm_b32", (const void*)k_perm_b32, 4},
+      {"v_fma_f64", (const void*)k_fma_f64, 8},       {"v_add_f64", (const void*)k_add_f64, 8},
+  };
+  const int iters = 4000;
+  printf("gfx950 VALU issue cost: shader cycles per wave64 instruction per SIMD (median over %d CUs, one block per CU)\n",
+         blocks);
+  printf("%-15s %10s %10s %10s\n", "instruction", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
+  std::vector<unsigned long long> h(blocks);
+  for (const K& k : ks) {
+    printf("%-15s", k.name);
+    for (int T : {256, 512, 1024}) {
+      void* args[] = {&out, &cyc, (void*)&iters};
+      (void)args;
+      for (int rep = 0; rep < 2; rep++) {
+        void* a[] = {&out, &cyc, const_cast<int*>(&iters)};
+        (void)hipLaunchKernel(k.fn, dim3(blocks), dim3(T), a, 0, 0);
+      }
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(h.data(), cyc, (size_t)blocks * 8, hipMemcpyDeviceToHost);
+      std::sort(h.begin(), h.end());
+      const double w = T / 256.0;
+      printf(" %10.2f", (double)h[blocks / 2] / (w * iters * 8.0));
+    }
+    printf("\n");
   }
   return 0;
 }

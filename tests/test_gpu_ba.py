@@ -260,12 +260,14 @@ def test_ba_medium_graph_vs_fp64_truth(mode):
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib"])
-def test_ba_full_chunk_runs_vs_fp64_truth(mode):
+def test_ba_full_chunk_runs_vs_fp64_truth(mode, monkeypatch):
     """6 keyframes at 128x192 = 24576 points per edge, one full linearisation chunk: every lane walks 48 point
     rounds, so the fp32 runs are flushed into the fp64 accumulators several times (the smaller graphs end
     inside the first run). Poses within 1e-5 of the oracle's fp64 truth."""
     from m3s.synthetic import make_graph, two_way
 
+    # the production chunk length of large graphs (small graphs get shorter chunks, abi.cpp ba_chunks)
+    monkeypatch.setenv("M3S_BA_CHUNK_POINTS", "24576")
     H, W = 128, 192
     G = make_graph(n_kf=6, H=H, W=W, seed=11)
     ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
@@ -307,3 +309,26 @@ def test_zero_copy_keyframe_plan_equals_stacked(golden):
     assert torch.equal(T_a, T_b) and torch.equal(dx_a, dx_b)
     with pytest.raises(RuntimeError):
         gauss_newton_sharded("rays", d(g["Twc0"]), None, None, *args, keyframes=(X_list, C_sum, [1, 0, 1, 1, 1, 1]))
+
+
+def test_rccl_all_reduce_path_equals_unsharded(tmp_path):
+    """The RCCL leg of the edge-sharded BA (m3s/dist_ba.py run_sharded: one dist.all_reduce of the fp64 edge-sum
+    table per GN iteration, replacing the reference's host loop gn_kernels.cu:1181-1225) executed on the GPU: a
+    fresh child process initialises the "nccl" (RCCL) process group at world size 1 before any other GPU call,
+    runs gauss_newton_sharded through the all-reduce, and must match the unsharded
+    mast3r_slam_backends.gauss_newton_rays bit for bit (tests/rccl_child.py)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-u", os.path.join(repo, "tests", "rccl_child.py")], env=env, cwd=repo,
+                       capture_output=True, text=True, timeout=240)
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "RCCL_BA_OK" in r.stdout

@@ -171,3 +171,56 @@ def test_track_recent_filtering_replaces_keyframe(golden):
     Xkf = torch.from_numpy(g["X"][1].reshape(-1, 3)).cuda()
     np.testing.assert_allclose(kf.X_canon.cpu().numpy(), T_CkCf.act(Xkf).cpu().numpy(), atol=2e-5, rtol=1e-5)
     assert kf.N == 1 and kf.N_updates == 2
+
+
+def test_track_while_ba_runs_on_another_stream():
+    """The reference runs the backend's global BA concurrently with tracking on the same GPU (main.py:268-269).
+    A 512x512 frame tracked while a K=64 chess-trajectory gauss_newton (30 iterations, enqueued first) occupies
+    the CUs from a second stream: the persistent GN launch's blocks become resident as the BA blocks drain and
+    the frame's pose, fused keyframe points and iteration count equal the solo run bit for bit; the BA result
+    equals its own solo run too."""
+    import mast3r_slam_backends as B
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, chess_poses, make_pair, make_traj_graph
+    from m3s.tracker import FrameTracker
+
+    config["use_calib"] = True
+    P = make_pair(512, 512, seed=4)
+    model = SyntheticModel([P], "cuda")
+
+    def track_once():
+        kf = Frame(0, (512, 512), T_WC=Sim3.Identity(1, device="cuda"))
+        kf.K = P["K"].cuda()
+        kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
+        kfs = Keyframes()
+        kfs.append(kf)
+        tr = FrameTracker(model, kfs, "cuda")
+        frame = Frame(1, (512, 512), T_WC=Sim3.Identity(1, device="cuda"))
+        new_kf, info, reloc = tr.track(frame)
+        assert not reloc
+        return frame.T_WC.data.clone(), kf.X_canon.clone(), kf.C.clone(), tr.last_result.iters
+
+    G = make_traj_graph(chess_poses(64), 384, 512, seed=1, device="cuda")
+    c = config["local_opt"]
+    ba_args = (G["Xs"].contiguous(), G["Cs"].contiguous(), G["ii"], G["jj"], G["idx"].contiguous(),
+               G["valid"].contiguous(), G["Q"].contiguous(), c["sigma_ray"], c["sigma_dist"], c["C_conf"],
+               c["Q_conf"], 30, 0.0)
+
+    def ba(stream):
+        T = G["Twc0"].clone()
+        with torch.cuda.stream(stream):
+            dx = B.gauss_newton_rays(T, *ba_args)[0]
+        return T, dx
+
+    solo = track_once()
+    s2 = torch.cuda.Stream()
+    T_ba_solo, dx_ba_solo = ba(s2)
+    torch.cuda.synchronize()
+    T_ba, dx_ba = ba(s2)  # enqueued: ~30 linearisation launches of ~500 edge blocks each on stream 2
+    both = track_once()   # meanwhile on the default stream
+    torch.cuda.synchronize()
+    for a, b in zip(solo, both):
+        assert (a == b) if isinstance(a, int) else torch.equal(a, b)
+    assert torch.equal(T_ba, T_ba_solo) and torch.equal(dx_ba, dx_ba_solo)
