@@ -359,3 +359,142 @@ def make_traj_graph(poses, H, W, loops_per_kf=3, seed=1, outlier_frac=0.05, vali
         Twc0[k] = _mul(dT, Twc0[k])
     return dict(Twc_gt=Twc_gt, Twc0=Twc0.to(dev), Xs=Xs.float(), Cs=Cs, ii=ii, jj=jj, idx=idx, valid=valid, Q=Q,
                 K=Kc, H=H, W=W, E_und=E_und)
+
+
+# ------------------------------------------------------------------------------------------------
+# backend replay (C3 / C4): a keyframe sequence with decoder outputs for any keyframe pair
+# ------------------------------------------------------------------------------------------------
+def _stable_seed(*key):
+    """A seed from a key tuple that does not depend on the interpreter's string-hash randomisation."""
+    import zlib
+
+    return zlib.crc32(repr(key).encode())
+
+
+class SceneReplay:
+    """Stands in for MASt3R + the retrieval model over a recorded trajectory, for replaying the backend loop
+    (main.py:116-165: retrieval -> add_factors -> solve_GN_* per new keyframe) without a checkpoint.
+
+    The world is the box room of ``make_traj_graph``. Keyframe k sees it from the ground-truth pose ``Twc_gt[k]``
+    (ray-cast pointmap, camera coordinates, + N(0, noise^2)); its initial pose ``Twc0[k]`` is the ground truth
+    perturbed (what tracking would hand the backend; keyframe 0 exact). Descriptors are a smooth 24-channel field
+    of the WORLD point (sums of random plane waves, L2-normalised), so the same surface point carries the same
+    descriptor in every view and the fused matcher finds the geometric correspondences.
+
+    * ``symmetric_inference(kfs_i, kfs_j)``: X, C, D, Q (4, b, H, W, ...) ordered (ii, ji, jj, ij) like
+      ``mast3r_decode_symmetric_batch`` (mast3r_utils.py:117-146): X_ji = T_i^-1 T_j X_j with ground-truth
+      poses, descriptors of the pixels' world points (+ noise).
+    * ``features(k)``: M local retrieval features of keyframe k (128-D, unit norm): a random unit vector per
+      coarse world voxel (0.5 m) that keyframe sees at M fixed pixels, + noise — the input of
+      ``RetrievalDatabase.quantize_custom``. The scoring around it (ASMK) is out of scope; ``retrieve`` ranks
+      earlier keyframes by shared visual words instead.
+    Keyframe ids are the frames' ``frame_id``."""
+
+    def __init__(self, poses, H, W, K=None, Fd=24, seed=3, noise=0.003, desc_noise=0.03,
+                 pose_noise=(0.01, 0.5, 0.005), n_feat=64, feat_dim=128, device="cpu"):
+        from m3s.sim3 import Sim3
+
+        dev = torch.device(device)
+        g = torch.Generator().manual_seed(seed)
+        P = torch.as_tensor(np.asarray(poses), dtype=torch.float64)
+        n_kf = P.shape[0]
+        centre = P[:, :3].mean(0)
+        self.half = float((P[:, :3] - centre).abs().max()) + 1.5
+        P[:, :3] -= centre
+        self.Twc_gt = P.float().to(dev)
+        self.H, self.W, self.N, self.dev = H, W, H * W, dev
+        self.K = (intrinsics(H, W) if K is None else torch.as_tensor(K, dtype=torch.float32)).to(dev)
+        fx, fy, cx, cy = [float(x) for x in (self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2])]
+        vv, uu = torch.meshgrid(torch.arange(H, dtype=torch.float32, device=dev),
+                                torch.arange(W, dtype=torch.float32, device=dev), indexing="ij")
+        rays = torch.stack(((uu - cx) / fx, (vv - cy) / fy, torch.ones_like(uu)), -1).reshape(-1, 3)
+        self.Xc, self.Xw = [], []
+        for k in range(n_kf):
+            T = Sim3(self.Twc_gt[k].view(1, 8))
+            d = _raycast_box(self.Twc_gt[k, :3], F.normalize(T.act(rays) - self.Twc_gt[k, :3], dim=-1), self.half)
+            Xc = rays * (d / rays.norm(dim=-1))[:, None]
+            self.Xc.append(Xc)
+            self.Xw.append(T.act(Xc))
+        # descriptor field: Fd channels, each a sum of 4 plane waves of 0.25-0.6 m wavelength
+        nw = 4
+        dirs = F.normalize(torch.randn(Fd, nw, 3, generator=g), dim=-1)
+        lam = 0.25 + 0.35 * torch.rand(Fd, nw, generator=g)
+        self.wave_k = (2 * math.pi * dirs / lam[..., None]).to(dev)
+        self.wave_ph = (2 * math.pi * torch.rand(Fd, nw, generator=g)).to(dev)
+        self.noise, self.desc_noise = noise, desc_noise
+        self.seed = seed
+        # per-keyframe confidences and pointmap noise (fixed per keyframe and view role)
+        self.C = [(1.0 + torch.empty(self.N).exponential_(0.25, generator=g)).to(dev) for _ in range(n_kf)]
+        t_n, r_n, s_n = pose_noise
+        Twc0 = self.Twc_gt.cpu().clone()
+        for k in range(1, n_kf):
+            dq = quat_from_axis_angle(torch.randn(3, generator=g).tolist(),
+                                      math.radians(r_n) * float(torch.randn(1, generator=g)))
+            dT = torch.cat((t_n * torch.randn(3, generator=g), dq,
+                            torch.tensor([1.0 + s_n * float(torch.randn(1, generator=g))])))
+            Twc0[k] = _mul(dT, Twc0[k])
+        self.Twc0 = Twc0.to(dev)
+        # retrieval features
+        self.n_feat, self.feat_dim = n_feat, feat_dim
+        self.feat_px = [torch.randperm(self.N, generator=g)[:n_feat].to(dev) for _ in range(n_kf)]
+
+    def _gen(self, *key):
+        return torch.Generator(device=self.dev).manual_seed(_stable_seed(self.seed, *key))
+
+    def descriptors(self, Xw, g):
+        ph = torch.einsum("fwc,nc->nfw", self.wave_k, Xw) + self.wave_ph[None]
+        D = torch.sin(ph).sum(-1)
+        D = D + self.desc_noise * torch.randn(D.shape, generator=g, device=self.dev)
+        return F.normalize(D, dim=-1)
+
+    def pointmap(self, k, role):
+        """Keyframe k's own pointmap as a decoder output of `role` (its own camera), with fresh noise."""
+        g = self._gen(k, role, "X")
+        return self.Xc[k] + self.noise * torch.randn(self.Xc[k].shape, generator=g, device=self.dev)
+
+    def keyframe(self, k):
+        """(X_canon (N,3), C (N,1)) the keyframe enters the backend with (its tracking-time canonical pointmap)."""
+        return self.pointmap(k, "kf"), self.C[k][:, None].clone()
+
+    def _rel(self, i, j, Xj):
+        from m3s.sim3 import Sim3
+
+        Tij = Sim3(self.Twc_gt[i].view(1, 8)).inv() * Sim3(self.Twc_gt[j].view(1, 8))
+        return Tij.act(Xj)
+
+    def symmetric_inference(self, kfs_i, kfs_j):
+        H, W = self.H, self.W
+        out = {n: [] for n in "XCDQ"}
+        for fi, fj in zip(kfs_i, kfs_j):
+            i, j = int(fi.frame_id), int(fj.frame_id)
+            Xii, Xjj = self.pointmap(i, ("ii", j)), self.pointmap(j, ("jj", i))
+            Xji = self._rel(i, j, self.pointmap(j, ("ji", i)))
+            Xij = self._rel(j, i, self.pointmap(i, ("ij", j)))
+            g = self._gen(i, j, "DQ")
+            Dii, Dji = self.descriptors(self.Xw[i], g), self.descriptors(self.Xw[j], g)
+            Djj, Dij = self.descriptors(self.Xw[j], g), self.descriptors(self.Xw[i], g)
+            for name, vals in (("X", (Xii, Xji, Xjj, Xij)), ("D", (Dii, Dji, Djj, Dij))):
+                out[name].append(torch.stack([v.reshape(H, W, -1) for v in vals]))
+            for name in "CQ":
+                out[name].append((1.0 + torch.empty(4, H, W, device=self.dev).exponential_(0.25, generator=g)))
+        return tuple(torch.stack(out[n], dim=1) for n in "XCDQ")
+
+    def features(self, k):
+        Xw = self.Xw[k][self.feat_px[k]]
+        cells = torch.floor(Xw / 0.5).long().cpu().tolist()
+        f = torch.stack([torch.randn(self.feat_dim, generator=torch.Generator().manual_seed(
+            _stable_seed(self.seed, "cell", *c))) for c in cells]).to(self.dev)
+        f = F.normalize(f, dim=-1)
+        g = self._gen(k, "feat")
+        return F.normalize(f + 0.1 * torch.randn(f.shape, generator=g, device=self.dev) / math.sqrt(self.feat_dim),
+                           dim=-1)
+
+
+def retrieve(words, k, n_best=3, min_thresh=5e-3):
+    """Earlier keyframes ranked by the fraction of keyframe k's visual words (quantize ids, (M, a)) they share
+    (a bag-of-words stand-in for the ASMK similarity of retrieval_database.py:106-170, which is out of scope);
+    the n_best with a score above min_thresh (main.py:121-126: retrieval k, min_thresh)."""
+    mine = set(np.asarray(words[k]).reshape(-1).tolist())
+    scores = [(len(mine & set(np.asarray(words[i]).reshape(-1).tolist())) / max(len(mine), 1), i) for i in range(k)]
+    scores.sort(key=lambda s: (-s[0], s[1]))
+    return [i for s, i in scores[:n_best] if s > min_thresh]

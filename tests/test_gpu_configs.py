@@ -124,24 +124,34 @@ def test_match_warm_start_at_c1_matches_oracle():
 SIG = {"rays": (0.003, 10.0), "calib": (1.0, 10.0)}
 
 
-@pytest.fixture(scope="module")
-def chess_graph():
-    from m3s.synthetic import chess_poses, make_traj_graph
+def _traj_graph(traj):
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
 
-    G = make_traj_graph(chess_poses(256), 48, 64, seed=1)
+    G = make_traj_graph((chess_poses if traj == "chess" else euroc_poses)(256), 48, 64, seed=1)
     return {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in G.items()}
 
 
+@pytest.fixture(scope="module")
+def chess_graph():
+    return _traj_graph("chess")
+
+
+@pytest.fixture(scope="module")
+def euroc_graph():
+    return _traj_graph("euroc")
+
+
 @pytest.mark.parametrize("solver", ["auto", "dense"])
-@pytest.mark.parametrize("mode", ["rays", "calib"])
-def test_ba_k256_chess_graph_vs_fp64_truth(chess_graph, mode, solver, monkeypatch):
-    """C4/C5-shaped global BA: 256 keyframes (255 optimised poses, n = 1785), ~2000 directed edges; the
-    plan's own choice of factorisation (block-sparse on this graph) and the dense fallback."""
+@pytest.mark.parametrize("mode,traj", [("rays", "chess"), ("calib", "chess"), ("rays", "euroc")])
+def test_ba_k256_graph_vs_fp64_truth(request, mode, traj, solver, monkeypatch):
+    """C4/C5-shaped global BA: 256 keyframes (255 optimised poses, n = 1785), ~2000 directed edges on the 7-Scenes
+    chess trajectory (C5; rays and calib) and the EuRoC MH_02 trajectory (C4, rays = config/eval_no_calib.yaml);
+    the plan's own choice of factorisation (block-sparse on these graphs) and the dense fallback."""
     import mast3r_slam_backends as B
 
     if solver != "auto":
         monkeypatch.setenv("M3S_BA_SOLVER", solver)
-    G = chess_graph
+    G = request.getfixturevalue(f"{traj}_graph")
     H, W = G["H"], G["W"]
     Xs = G["Xs"] if mode == "rays" else O.backproject_constrain(G["Xs"], G["K"], (H, W))
     sa, sb = SIG[mode]
@@ -159,7 +169,8 @@ def test_ba_k256_chess_graph_vs_fp64_truth(chess_graph, mode, solver, monkeypatc
         dx = B.gauss_newton_calib(T, Xs_, Cs_, c(G["K"]), ii_, jj_, idx_, v_, Q_, H, W, -10, 1e-6, sa, sb, 0.0, 1.5,
                                   10, 1e-8)[0]
     T, dx = T.cpu().numpy(), dx.cpu().numpy()
-    print(f"K=256 {mode}: pose err vs fp64 truth {np.abs(T - T_ref).max():.2e}, |dx_ref| {np.linalg.norm(dx_ref):.2e}")
+    print(f"K=256 {traj} {mode} {solver}: pose err vs fp64 truth {np.abs(T - T_ref).max():.2e}, "
+          f"|dx_ref| {np.linalg.norm(dx_ref):.2e}")
     assert dx.shape == (255, 7)
     np.testing.assert_allclose(T, T_ref, atol=1e-5)
     np.testing.assert_allclose(dx, dx_ref, atol=1e-5)

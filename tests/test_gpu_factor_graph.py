@@ -165,3 +165,82 @@ def test_c3_backend_chain(monkeypatch):
     got = np.stack([kfs[k].T_WC.data.cpu().numpy()[0] for k in range(2)])
     assert np.isfinite(got).all()
     np.testing.assert_allclose(got, T_ref, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,traj", [("calib", "chess"), ("rays", "euroc")])
+def test_backend_replay_growing_graph_vs_fp64_truth(mode, traj, monkeypatch):
+    """The backend loop of main.py:116-155 replayed over 20 keyframes (C3: 7-Scenes chess trajectory, calib mode,
+    TUM fr1 K at 120x160; C4: EuRoC MH_02 trajectory, rays mode): for every new keyframe its retrieval features
+    are quantized on the matrix cores (checked against the reference's quantize_custom restated), earlier keyframes
+    are retrieved by shared visual words (ASMK scoring is out of scope), the consecutive + retrieved loop edges go
+    through FactorGraph.add_factors (fused symmetric matching on SceneReplay's decoder outputs) and
+    solve_GN_calib / solve_GN_rays runs on the grown graph. After EVERY call the poses must sit within 1e-5 of the
+    oracle's fp64 truth run on the same graph tensors (SURVEY §8c a-note 6)."""
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.geometry import constrain_points_to_ray
+    from m3s.global_opt import FactorGraph
+    from m3s.retrieval import Codebook
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SceneReplay, chess_poses, euroc_poses, intrinsics, retrieve, tum_fr1_intrinsics
+
+    calib = mode == "calib"
+    monkeypatch.setitem(config, "use_calib", calib)
+    dev = torch.device("cuda")
+    n_kf, H, W = 20, 120, 160
+    K = tum_fr1_intrinsics(H, W) if calib else intrinsics(H, W)
+    S = SceneReplay((chess_poses if traj == "chess" else euroc_poses)(n_kf), H, W, K=K, device=dev)
+    kfs = Keyframes()
+    Kd = K.to(dev)
+    fg = FactorGraph(S, kfs, K=Kd, device=dev)
+    rng = np.random.default_rng(11)
+    cent = rng.standard_normal((2048, 128)).astype(np.float32)
+    cent /= np.linalg.norm(cent, axis=1, keepdims=True)
+    cb = Codebook(torch.from_numpy(cent).to(dev))
+    c = config["local_opt"]
+    sa, sb = (c["sigma_pixel"], c["sigma_depth"]) if calib else (c["sigma_ray"], c["sigma_dist"])
+    p = O.ba_params(mode, sa, sb, c["C_conf"], c["Q_conf"], K=K.numpy(), height=H, width=W,
+                    pixel_border=c["pixel_border"], z_eps=c["depth_eps"])
+    words, loops, errs = {}, 0, []
+    for idx in range(n_kf):
+        X, C = S.keyframe(idx)
+        f = Frame(idx, (H, W), T_WC=Sim3(S.Twc0[idx].view(1, 8).clone()))
+        f.K = Kd
+        f.update_pointmap(X, C)
+        kfs.append(f)
+        q = S.features(idx)
+        ids = cb.quantize(q, 5).cpu().numpy()
+        ref_ids, l2 = O.quantize_custom(cent, q.cpu().numpy(), 5)
+        assert O.topk_equivalent(ids, ref_ids, l2, 1e-4).all()
+        words[idx] = ids
+        if idx == 0:
+            continue
+        retrieved = retrieve(words, idx, config["retrieval"]["k"], config["retrieval"]["min_thresh"])
+        kf_idx = sorted(set([idx - 1] + retrieved) - {idx})  # main.py:117-141
+        loops += len(set(retrieved) - {idx - 1})
+        fg.add_factors(kf_idx, [idx] * len(kf_idx), c["min_match_frac"])
+        # the fp64 truth on the graph's own tensors, from the poses the solve starts at
+        uniq = fg.get_unique_kf_idx()
+        Xg, T_WCs, Cg = fg.get_poses_points(uniq)
+        if calib:
+            Xg = constrain_points_to_ray((H, W), Xg, Kd)
+        ii, jj, idx2, valid, Qe = fg.prep_two_way_edges()
+        T_ref, _, _ = O.gauss_newton_f64(mode, T_WCs.data[:, 0, :].cpu().numpy().astype(np.float64),
+                                         Xg.cpu().numpy().astype(np.float64),
+                                         Cg.cpu().numpy()[..., 0].astype(np.float64), ii.cpu().numpy(),
+                                         jj.cpu().numpy(), idx2.cpu().numpy(), valid.cpu().numpy()[..., 0],
+                                         Qe.cpu().numpy()[..., 0].astype(np.float64), p, c["max_iters"],
+                                         c["delta_norm"])
+        (fg.solve_GN_calib if calib else fg.solve_GN_rays)()
+        got = np.stack([kfs[int(k)].T_WC.data.cpu().numpy()[0] for k in uniq.tolist()])
+        assert np.isfinite(got).all()
+        errs.append(float(np.abs(got - T_ref).max()))
+        np.testing.assert_allclose(got, T_ref, atol=1e-5, err_msg=f"after keyframe {idx}")
+    print(f"replay {traj} {mode}: {fg.ii.numel()} edges ({loops} retrieved loop edges), max pose error vs fp64 "
+          f"truth per call: max {max(errs):.2e}")
+    assert loops > 0
+    # the optimised trajectory is closer to the ground truth than the initial one
+    T_fin = np.stack([kfs[k].T_WC.data.cpu().numpy()[0] for k in range(n_kf)])
+    gt, t0 = S.Twc_gt.cpu().numpy(), S.Twc0.cpu().numpy()
+    assert np.abs(T_fin[:, :3] - gt[:, :3]).mean() < np.abs(t0[:, :3] - gt[:, :3]).mean()
