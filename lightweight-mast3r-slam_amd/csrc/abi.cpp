@@ -7,7 +7,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -453,13 +455,11 @@ struct BaPlanImpl {
   BaArgs a;
   BaParams p;
   int Kp, N, E, e0, e1;
-  int nL;
-  int step_tasks[BA_MAX_WIDE_STEPS];  // tasks (waves) of each multi-workgroup factor step
-  int dense;  // 1: the dense fallback factorisation (ba_dense.hip)
   int n_targets;  // distinct target keyframes j among this shard's edges (their X_j slabs are streamed per iteration)
   float delta_thresh;
   size_t edge_sums_off, edge_sums_bytes;
   void* ws;
+  unsigned long long sym_gen;  // the PlanSym (symbolic half) this plan owns, by generation
 };
 static_assert(sizeof(BaPlanImpl) <= sizeof(m3s_ba_plan), "m3s_ba_plan too small");
 
@@ -582,6 +582,170 @@ extern "C" int m3s_ba_pattern_stats(const int64_t* ii, const int64_t* jj, int E,
 }
 
 namespace {
+// The symbolic half of a plan (ordering, factor pattern, levels, update groups, assembly CSR; ba_pattern.h) and
+// the solve schedule derived from it. It is needed only from the first m3s_ba_solve on, so it is built on a host
+// worker thread while the device packs the point records and runs the first linearisation: the host analysis
+// (~0.6 ms at K = 256) leaves the replicated, unsharded part of a multi-GPU solve. m3s_ba_solve (or
+// m3s_ba_plan_info) joins it once and uploads its tables. One per workspace (a new plan on the same workspace
+// first joins the previous one); `gen` ties a plan to it.
+struct PlanSym {
+  unsigned long long gen = 0;
+  std::future<int> fut;
+  bool joined = false, uploaded = false;
+  int rc = M3S_OK;
+  std::string err;
+  // worker output (read by the main thread only after the join)
+  std::vector<char> image;  // the tables, packed at 16-B aligned offsets, as uploaded
+  size_t off[14] = {0};
+  int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, plan_lo_off = 0, plan_bytes = 0;
+  int step_tasks[BA_MAX_WIDE_STEPS] = {0};
+  char* dst = nullptr;  // device destination (the blob region after the plan's own tables)
+};
+std::mutex g_sym_mu;
+std::map<const void*, std::unique_ptr<PlanSym>> g_sym;  // by workspace
+unsigned long long g_sym_gen = 0;
+
+// worker: ranks ri / rj (all E edges) -> the packed symbolic tables and the factor schedule
+int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, int Kp, bool has_dense,
+                   size_t capacity) {
+  BaPattern S;
+  ba_build_pattern(ri.data(), rj.data(), E, Kp, &S, ba_max_pairs(Kp));
+  if (S.too_dense || S.sidx.size() > ba_max_pairs(Kp)) {
+    Y->err = "ba: factor pattern too dense for the plan tables";
+    return M3S_EINVAL;
+  }
+  const std::vector<int>* secs[14] = {&S.perm, &S.col_ptr, &S.rowL, &S.lev_ptr, &S.lev_col, &S.grp_ptr, &S.grp,
+                                      &S.pull_grp, &S.src, &S.sidx, &S.asm_ptr, &S.asm_ent, &S.rhs_ptr, &S.rhs_ent};
+  size_t total = 0;
+  for (int k = 0; k < 14; k++) {
+    Y->off[k] = total;
+    total += (sizeof(int) * secs[k]->size() + 15) & ~(size_t)15;
+  }
+  if (total > capacity) {
+    Y->err = "ba: factor pattern too dense for the plan tables";
+    return M3S_EINVAL;
+  }
+  Y->image.assign(total, 0);
+  for (int k = 0; k < 14; k++)
+    if (!secs[k]->empty()) memcpy(Y->image.data() + Y->off[k], secs[k]->data(), sizeof(int) * secs[k]->size());
+  Y->nb = S.nb;
+  Y->nlev = S.nlev;
+  Y->nL = S.nL;
+  Y->plan_lo_off = (int)Y->off[1];  // col_ptr .. sidx, staged into LDS by the factor kernel
+  Y->plan_bytes = (int)(Y->off[9] + S.sidx.size() * sizeof(int) - Y->off[1]);
+  // sparse or dense factorisation: measured on MI355X (scripts/ba_exp.py), the one-workgroup sparse
+  // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
+  // update volume); the dense one ~2.7 us per pose (its pivot chain)
+  Y->dense = has_dense && 3.8 * S.nlev + 0.03 * (double)S.sidx.size() > 2.7 * S.nb;
+  if (const char* f = getenv("M3S_BA_SOLVER")) {  // tests and experiments: force one factorisation
+    if (!strcmp(f, "sparse")) Y->dense = 0;
+    if (!strcmp(f, "dense") && has_dense) Y->dense = 1;
+  }
+  // the leaf end of the elimination tree runs as multi-workgroup launches (steps [0, wide_steps)), the root end
+  // in the one-workgroup kernel. The split minimises the measured step costs (MI355X, C5/C4 graphs): a launch
+  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of 16 waves (one wave per task).
+  // M3S_BA_WIDE=t (tests, experiments): every step up to the last one with more than t tasks instead.
+  std::vector<int> tasks(S.nlev + 1);
+  for (int l = 0; l <= S.nlev; l++) {
+    const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
+    tasks[l] = na + S.grp_ptr[l + 1] - S.grp_ptr[l];
+    if (l < BA_MAX_WIDE_STEPS) Y->step_tasks[l] = tasks[l];
+  }
+  const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
+  if (const char* w = getenv("M3S_BA_WIDE")) {
+    const int thr = atoi(w);
+    int last = -1;
+    for (int l = 0; l <= S.nlev; l++)
+      if (tasks[l] > thr) last = l;
+    Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+  } else {
+    constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
+    std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
+    for (int l = lmax - 1; l >= 0; l--) suffix[l] = suffix[l + 1] + kRoundUs * ((tasks[l] + 15) / 16);
+    int best_L = 0;
+    double best = suffix[0];
+    for (int L = 1; L <= lmax; L++) {
+      const double c = kLaunchUs * L + suffix[L];
+      if (c < best) {
+        best = c;
+        best_L = L;
+      }
+    }
+    Y->wide_steps = best_L;
+  }
+  return M3S_OK;
+}
+
+// the plan's PlanSym, joined (with `upload`, its tables enqueued on `s` the first time); nullptr + g_err on failure
+PlanSym* plan_symbolic(const BaPlanImpl* P, hipStream_t s, bool upload, int* rc) {
+  std::lock_guard<std::mutex> lock(g_sym_mu);
+  auto it = g_sym.find(P->ws);
+  if (it == g_sym.end() || it->second->gen != P->sym_gen) {
+    *rc = fail(M3S_EINVAL, "ba: this plan was superseded by a newer plan on the same workspace");
+    return nullptr;
+  }
+  PlanSym* Y = it->second.get();
+  if (!Y->joined) {
+    Y->rc = Y->fut.get();
+    Y->joined = true;
+  }
+  if (upload && !Y->uploaded && Y->rc == M3S_OK) {
+    Y->uploaded = true;
+    if (!Y->image.empty()) {
+      PlanStage& st = plan_stage();
+      std::lock_guard<std::mutex> sl(st.mu);
+      hipError_t e = hipSuccess;
+      if (st.pending) e = hipEventSynchronize(st.landed);
+      st.pending = false;
+      if (e == hipSuccess && !st.landed) e = hipEventCreateWithFlags(&st.landed, hipEventDisableTiming);
+      if (e == hipSuccess && st.cap < Y->image.size()) {
+        if (st.buf) (void)hipHostFree(st.buf);
+        st.buf = nullptr;
+        st.cap = 0;
+        const size_t want = std::max(Y->image.size(), (size_t)1 << 20);
+        e = hipHostMalloc((void**)&st.buf, want, hipHostMallocDefault);
+        if (e == hipSuccess) st.cap = want;
+      }
+      if (e == hipSuccess) {
+        memcpy(st.buf, Y->image.data(), Y->image.size());
+        e = hipMemcpyAsync(Y->dst, st.buf, Y->image.size(), hipMemcpyHostToDevice, s);
+      }
+      if (e == hipSuccess) e = hipEventRecord(st.landed, s);
+      if (e != hipSuccess) {
+        Y->rc = M3S_EHIP;
+        Y->err = std::string("ba symbolic upload: ") + hipGetErrorString(e);
+      } else {
+        st.pending = true;
+      }
+      std::vector<char>().swap(Y->image);
+    }
+  }
+  if (Y->rc != M3S_OK) {
+    *rc = fail(Y->rc, Y->err);
+    return nullptr;
+  }
+  *rc = M3S_OK;
+  return Y;
+}
+
+// P->a with the symbolic tables of Y
+BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
+  BaArgs a = P->a;
+  const char* d = Y->dst;
+  const void** dst[14] = {(const void**)&a.perm, (const void**)&a.col_ptr, (const void**)&a.rowL,
+                          (const void**)&a.lev_ptr, (const void**)&a.lev_col, (const void**)&a.grp_ptr,
+                          (const void**)&a.grp, (const void**)&a.pull_grp, (const void**)&a.src,
+                          (const void**)&a.sidx, (const void**)&a.asm_ptr, (const void**)&a.asm_ent,
+                          (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent};
+  for (int k = 0; k < 14; k++) *dst[k] = d + Y->off[k];
+  a.plan_lo = d + Y->plan_lo_off;
+  a.plan_bytes = Y->plan_bytes;
+  a.nb = Y->nb;
+  a.nlev = Y->nlev;
+  a.wide_steps = Y->wide_steps;
+  return a;
+}
+
 // Keyframe sources (host arrays of Kp entries) -> the plan's device tables.
 int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* Xh, const float* const* Ch,
                       const float* scale_h, int Kp, int N, const int64_t* ii, const int64_t* jj, int E, int e0, int e1,
@@ -605,6 +769,17 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   void* blob;
   ba_carve(c, Kp, N, E, chunks, &P.a, &P.edge_sums_off, &blob);
   P.edge_sums_bytes = (size_t)E * 36 * sizeof(double);
+  // a previous plan on this workspace: its worker must be done before the workspace is rewritten
+  PlanSym* Y = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_sym_mu);
+    auto& slot = g_sym[workspace];
+    if (slot && !slot->joined && slot->fut.valid()) slot->fut.wait();
+    slot.reset(new PlanSym());
+    Y = slot.get();
+    Y->gen = ++g_sym_gen;
+    P.sym_gen = Y->gen;
+  }
   // rank remap (gn_kernels.cu:161-170): unique(cat(ii,jj)) sorted; searchsorted; pin = 1 for rows
   std::vector<int64_t> hii(E), hjj(E);
   if (E > 0) {
@@ -622,10 +797,6 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     ri[e] = (int)(std::lower_bound(u.begin(), u.end(), hii[e]) - u.begin());
     rj[e] = (int)(std::lower_bound(u.begin(), u.end(), hjj[e]) - u.begin());
   }
-  // symbolic factorisation of the pose system (SparseBlock's pattern, gn_kernels.cu:71-113)
-  BaPattern S;
-  ba_build_pattern(ri.data(), rj.data(), E, Kp, &S, ba_max_pairs(Kp));
-  if (S.too_dense) return fail(M3S_EINVAL, "ba: factor pattern too dense for the plan tables");
   // linearisation block table: this shard's edges grouped by target keyframe j, chunk-major within a
   // group, so consecutive blocks (dealt to one XCD by xcd_remap) read the same X_j slab
   std::vector<int> lin_tab;
@@ -646,7 +817,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     std::vector<char> seen(Kp, 0);
     for (int e = e0; e < e1; e++) P.n_targets += seen[rj[e]] ? 0 : (seen[rj[e]] = 1);
   }
-  // pack every table into one staging image of the device blob
+  // the tables the pack and the linearisation read, in ONE upload ahead of the pack; the symbolic tables follow
+  // in the same blob (their own upload, at the first solve)
   struct Sec {
     const void* src;
     size_t bytes;
@@ -658,27 +830,13 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       {Xh, sizeof(const float*) * Kp, (const void**)&P.a.Xkf},
       {Ch, sizeof(const float*) * Kp, (const void**)&P.a.Ckf},
       {scale_h, sizeof(float) * Kp, (const void**)&P.a.Cscale},
-      {S.perm.data(), sizeof(int) * S.perm.size(), (const void**)&P.a.perm},
-      {S.col_ptr.data(), sizeof(int) * S.col_ptr.size(), (const void**)&P.a.col_ptr},
-      {S.rowL.data(), sizeof(int) * S.rowL.size(), (const void**)&P.a.rowL},
-      {S.lev_ptr.data(), sizeof(int) * S.lev_ptr.size(), (const void**)&P.a.lev_ptr},
-      {S.lev_col.data(), sizeof(int) * S.lev_col.size(), (const void**)&P.a.lev_col},
-      {S.grp_ptr.data(), sizeof(int) * S.grp_ptr.size(), (const void**)&P.a.grp_ptr},
-      {S.grp.data(), sizeof(int) * S.grp.size(), (const void**)&P.a.grp},
-      {S.pull_grp.data(), sizeof(int) * S.pull_grp.size(), (const void**)&P.a.pull_grp},
-      {S.src.data(), sizeof(int) * S.src.size(), (const void**)&P.a.src},
-      {S.sidx.data(), sizeof(int) * S.sidx.size(), (const void**)&P.a.sidx},
-      {S.asm_ptr.data(), sizeof(int) * S.asm_ptr.size(), (const void**)&P.a.asm_ptr},
-      {S.asm_ent.data(), sizeof(int) * S.asm_ent.size(), (const void**)&P.a.asm_ent},
-      {S.rhs_ptr.data(), sizeof(int) * S.rhs_ptr.size(), (const void**)&P.a.rhs_ptr},
-      {S.rhs_ent.data(), sizeof(int) * S.rhs_ent.size(), (const void**)&P.a.rhs_ent},
       {lin_tab.data(), sizeof(int) * lin_tab.size(), (const void**)&P.a.lin_tab},
   };
-  static_assert(sizeof(secs) / sizeof(secs[0]) == BA_BLOB_SECTIONS, "blob sections");
+  static_assert(sizeof(secs) / sizeof(secs[0]) + 14 == BA_BLOB_SECTIONS, "blob sections");
   size_t total = 0;
   for (const Sec& x : secs) total += (x.bytes + 15) & ~(size_t)15;
-  if (S.sidx.size() > ba_max_pairs(Kp) || total > ba_blob_capacity(Kp, E, chunks))
-    return fail(M3S_EINVAL, "ba: factor pattern too dense for the plan tables");
+  const size_t capacity = ba_blob_capacity(Kp, E, chunks);
+  if (total > capacity) return fail(M3S_EINVAL, "ba: plan tables exceed the workspace blob");
   {
     PlanStage& st = plan_stage();
     std::lock_guard<std::mutex> lock(st.mu);
@@ -703,56 +861,10 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     HIP_TRY(hipEventRecord(st.landed, s), "ba stage record");
     st.pending = true;
   }
+  Y->dst = static_cast<char*>(blob) + total;
   HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
   HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");
-  // sparse or dense factorisation: measured on MI355X (scripts/ba_exp.py), the one-workgroup sparse
-  // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
-  // update volume); the dense one ~2.7 us per pose (its pivot chain)
-  P.dense = P.a.H != nullptr && 3.8 * S.nlev + 0.03 * (double)S.sidx.size() > 2.7 * S.nb;
-  if (const char* f = getenv("M3S_BA_SOLVER")) {  // tests and experiments: force one factorisation
-    if (!strcmp(f, "sparse")) P.dense = 0;
-    if (!strcmp(f, "dense") && P.a.H) P.dense = 1;
-  }
-  // the leaf end of the elimination tree runs as multi-workgroup launches (steps [0, wide_steps)), the root end
-  // in the one-workgroup kernel. The split minimises the measured step costs (MI355X, C5/C4 graphs): a launch
-  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of 16 waves (one wave per task).
-  // M3S_BA_WIDE=t (tests, experiments): every step up to the last one with more than t tasks instead.
-  {
-    std::vector<int> tasks(S.nlev + 1);
-    for (int l = 0; l <= S.nlev; l++) {
-      const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
-      tasks[l] = na + S.grp_ptr[l + 1] - S.grp_ptr[l];
-      if (l < BA_MAX_WIDE_STEPS) P.step_tasks[l] = tasks[l];
-    }
-    const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
-    if (const char* w = getenv("M3S_BA_WIDE")) {
-      const int thr = atoi(w);
-      int last = -1;
-      for (int l = 0; l <= S.nlev; l++)
-        if (tasks[l] > thr) last = l;
-      P.a.wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
-    } else {
-      constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
-      std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
-      for (int l = lmax - 1; l >= 0; l--) suffix[l] = suffix[l + 1] + kRoundUs * ((tasks[l] + 15) / 16);
-      int best_L = 0;
-      double best = suffix[0];
-      for (int L = 1; L <= lmax; L++) {
-        const double c = kLaunchUs * L + suffix[L];
-        if (c < best) {
-          best = c;
-          best_L = L;
-        }
-      }
-      P.a.wide_steps = best_L;
-    }
-  }
   P.a.bad = P.a.info + 3;
-  P.a.plan_lo = reinterpret_cast<const char*>(P.a.col_ptr);
-  P.a.plan_bytes = (int)(reinterpret_cast<const char*>(P.a.sidx) + S.sidx.size() * sizeof(int) - P.a.plan_lo);
-  P.a.nb = S.nb;
-  P.a.nlev = S.nlev;
-  P.nL = S.nL;
   P.a.Twc = Twc;
   P.a.idx = idx;
   P.a.valid = valid;
@@ -788,6 +900,10 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     Span sp("ba_pack", s);
     HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
   }
+  // the symbolic analysis of ALL E edges (every rank builds the identical system) runs on a host worker while
+  // the device packs and linearises
+  Y->fut = std::async(std::launch::async, build_symbolic, Y, std::move(ri), std::move(rj), E, Kp, P.a.H != nullptr,
+                      capacity - total);
   memcpy(plan->opaque, &P, sizeof(P));
   return M3S_OK;
 }
@@ -834,11 +950,14 @@ extern "C" int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, si
 extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   M3S_CHECK(plan && info, "ba: null argument");
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  int rc;
+  const PlanSym* Y = plan_symbolic(P, nullptr, false, &rc);  // joins the symbolic analysis
+  if (Y == nullptr) return rc;
   info[0] = P->p.chunks;
-  info[1] = P->nL;
-  info[2] = P->a.nlev;
-  info[3] = P->a.wide_steps;
-  info[4] = P->dense;
+  info[1] = Y->nL;
+  info[2] = Y->nlev;
+  info[3] = Y->wide_steps;
+  info[4] = Y->dense;
   info[5] = P->n_targets;
   info[6] = P->e1 - P->e0;
   info[7] = P->Kp;
@@ -860,9 +979,14 @@ extern "C" int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream) {
 extern "C" int m3s_ba_solve(const m3s_ba_plan* plan, void* stream) {
   M3S_CHECK(plan, "ba: null plan");
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
-  Span sp("ba_solve", (hipStream_t)stream);
-  HIP_TRY(P->dense ? m3s_launch_ba_solve_dense(&P->a, P->Kp, P->nL, P->delta_thresh, (hipStream_t)stream)
-                   : m3s_launch_ba_solve(&P->a, P->Kp, P->nL, P->delta_thresh, P->step_tasks, (hipStream_t)stream),
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  const PlanSym* Y = plan_symbolic(P, s, true, &rc);  // the first solve joins the host worker and uploads its tables
+  if (Y == nullptr) return rc;
+  const BaArgs a = with_symbolic(P, Y);
+  Span sp("ba_solve", s);
+  HIP_TRY(Y->dense ? m3s_launch_ba_solve_dense(&a, P->Kp, Y->nL, P->delta_thresh, s)
+                   : m3s_launch_ba_solve(&a, P->Kp, Y->nL, P->delta_thresh, Y->step_tasks, s),
           "ba solve launch");
   return M3S_OK;
 }
