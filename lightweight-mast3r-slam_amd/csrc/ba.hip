@@ -140,6 +140,24 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
   }
 }
 
+#ifdef BA_V_RUN  // (experiment) a shorter fp32 run for the 7 gradient sums only: the odd lane owns them (18..34)
+__device__ __forceinline__ void pair_flush_v(double* acc, f2* fv, bool odd) {
+#pragma unroll
+  for (int c = 28; c < 35; c++) {
+    const int m = c - BA_PAIR_HALF;
+    const f2 own = fv[c - 28];
+    const f2 got = {dpp_swap1(own.x), dpp_swap1(own.y)};
+    if (odd) {
+      acc[m] += (double)own.x;
+      acc[m] += (double)own.y;
+      acc[m] += (double)got.x;
+      acc[m] += (double)got.y;
+    }
+    fv[c - 28] = f2{0.0f, 0.0f};
+  }
+}
+#endif
+
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
 //   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
 //   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
@@ -300,6 +318,9 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
     }
+#if defined(BA_V_RUN) && BA_PAIR_ACC
+    if ((run + 1) % BA_V_RUN == 0 && run + 1 != BA_RUN_LEN) pair_flush_v(acc, fv, odd);
+#endif
     if (++run == BA_RUN_LEN) {  // the run's fp32 sums (BA_RUN_LEN points per slot) into the fp64 accumulators
       run = 0;
 #if BA_PAIR_ACC

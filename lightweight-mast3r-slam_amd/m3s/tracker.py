@@ -57,15 +57,18 @@ _K_CACHE = {}
 
 
 def _host_K(K):
-    """Host copy of the intrinsics, cached per tensor version: a device->host read every frame would
-    serialise the host against the matcher kernels still in flight."""
-    key = (K.data_ptr(), K._version, str(K.device))
-    Kh = _K_CACHE.get(key)
-    if Kh is None:
-        Kh = K.detach().float().cpu().reshape(-1).tolist()
-        if len(_K_CACHE) > 64:
-            _K_CACHE.clear()
-        _K_CACHE[key] = Kh
+    """Host copy of the intrinsics, cached per live tensor and version: a device->host read every frame would
+    serialise the host against the matcher kernels still in flight. The entry holds a weak reference to the
+    tensor it was read from, so a new tensor that reuses a freed one's address (or Python id) never hits."""
+    import weakref
+
+    e = _K_CACHE.get(id(K))
+    if e is not None and e[0]() is K and e[1] == K._version and e[2] == K.data_ptr():
+        return e[3]
+    Kh = K.detach().float().cpu().reshape(-1).tolist()
+    if len(_K_CACHE) > 64:
+        _K_CACHE.clear()
+    _K_CACHE[id(K)] = (weakref.ref(K), K._version, K.data_ptr(), Kh)
     return Kh
 
 
@@ -122,7 +125,7 @@ class FrameTracker:
     def _config(self, use_calib, img_size, K, max_iters):
         """m3s_track_config, rebuilt only when the inputs that shape it change."""
         cfg = self.cfg
-        kkey = None if (K is None or not use_calib) else (K.data_ptr(), K._version)
+        kkey = None if (K is None or not use_calib) else tuple(_host_K(K))  # the values (a freed K's address can recur)
         key = (use_calib, tuple(img_size), kkey, max_iters, tuple(cfg.items()))
         if getattr(self, "_cfg_key", None) != key:
             c = dict(cfg)

@@ -30,13 +30,18 @@
     const T k = (T)1;                                                                                 \
     __syncthreads();                                                                                  \
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();                                       \
+    const unsigned long long r0t = __builtin_amdgcn_s_memrealtime();                                  \
     for (int i = 0; i < iters; i++) {                                                                 \
       BODY8(ASM)                                                                                      \
     }                                                                                                 \
     __syncthreads();                                                                                  \
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();                                       \
+    const unsigned long long r1t = __builtin_amdgcn_s_memrealtime();                                  \
     out[blockIdx.x * blockDim.x + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;               \
-    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                                  \
+    if (threadIdx.x == 0) {                                                                           \
+      cyc[blockIdx.x] = t1 - t0;                                                                      \
+      cyc[gridDim.x + blockIdx.x] = r1t - r0t;                                                        \
+    }                                                                                                 \
   }
 
 // 32-bit operand instructions (f16 / packed f16 / packed-f32 halves live in 32-bit VGPRs)
@@ -65,7 +70,7 @@ int main() {
   void* out;
   unsigned long long* cyc;
   (void)hipMalloc(&out, (size_t)blocks * 1024 * 8);
-  (void)hipMalloc(&cyc, (size_t)blocks * 8);
+  (void)hipMalloc(&cyc, (size_t)blocks * 16);
   struct K {
     const char* name;
     const void* fn;
@@ -81,10 +86,10 @@ int main() {
       {"v_fma_f64", (const void*)k_fma_f64, 8},       {"v_add_f64", (const void*)k_add_f64, 8},
   };
   const int iters = 4000;
-  printf("gfx950 VALU issue cost: shader cycles per wave64 instruction per SIMD (median over %d CUs, one block per CU)\n",
-         blocks);
-  printf("%-15s %10s %10s %10s\n", "instruction", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
-  std::vector<unsigned long long> h(blocks);
+  printf("gfx950 VALU issue cost per wave64 instruction per SIMD (median over %d CUs, one block per CU):\n"
+         "s_memtime cycles | ns (s_memrealtime, 100 MHz) | cycles at 2.4 GHz from the ns\n", blocks);
+  printf("%-15s %26s %26s %26s\n", "instruction", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
+  std::vector<unsigned long long> h(2 * blocks), hc(blocks), hr(blocks);
   for (const K& k : ks) {
     printf("%-15s", k.name);
     for (int T : {256, 512, 1024}) {
@@ -95,10 +100,16 @@ int main() {
         (void)hipLaunchKernel(k.fn, dim3(blocks), dim3(T), a, 0, 0);
       }
       (void)hipDeviceSynchronize();
-      (void)hipMemcpy(h.data(), cyc, (size_t)blocks * 8, hipMemcpyDeviceToHost);
-      std::sort(h.begin(), h.end());
-      const double w = T / 256.0;
-      printf(" %10.2f", (double)h[blocks / 2] / (w * iters * 8.0));
+      (void)hipMemcpy(h.data(), cyc, (size_t)blocks * 16, hipMemcpyDeviceToHost);
+      for (int b = 0; b < blocks; b++) {
+        hc[b] = h[b];
+        hr[b] = h[blocks + b];
+      }
+      std::sort(hc.begin(), hc.end());
+      std::sort(hr.begin(), hr.end());
+      const double w = T / 256.0, n = w * iters * 8.0;
+      const double ns = (double)hr[blocks / 2] * 10.0 / n;
+      printf("   %7.2f | %6.3f | %6.2f", (double)hc[blocks / 2] / n, ns, ns * 2.4);
     }
     printf("\n");
   }
