@@ -758,7 +758,21 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
     }
   }
   if (fail && lane == 0) *bad = 1;
-  if (lane < 7) {  // 1/L_mm in column 7 of the diagonal block (used by the back substitution)
+  if (lane < 7) {
+    // L_jj^-1 for the back substitution, off its chain: lane c forward-substitutes e_c (column c of the inverse,
+    // zero above row c) and keeps (L_jj^-1)[i][c], i > c, in the strictly upper part of its own row of the
+    // diagonal block (block[c][i], unused by the factorisation) and 1/L_cc = (L_jj^-1)[c][c] in column 7
+    double col[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      double acc = lane == i ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; k++) acc = fma(-lo[i * (i - 1) / 2 + k], col[k], acc);
+      col[i] = acc * inv[i];
+    }
+#pragma unroll
+    for (int i = 1; i < 7; i++)
+      if (i > lane) v1[i] = col[i];
     double iv = inv[0];
 #pragma unroll
     for (int m = 1; m < 7; m++) iv = lane == m ? inv[m] : iv;
@@ -788,24 +802,46 @@ __device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables&
 }
 
 // back substitution of column j: x_j = L_jj^-T (y_j - sum_{i in struct(j)} L_ij^T x_i); X = the solution
-// (LDS when it fits), 8 doubles per column
-__device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& T, double* X, int j, int lane,
-                                               double* red) {
+// (LDS when it fits), 8 doubles per column. Everything it reads from the factor is final before the back
+// substitution starts, so a wave loads its NEXT column's data (SpBack) while it solves the current one: only
+// the x_i of the ancestors (LDS) sit on the level-to-level chain.
+struct SpBack {
+  double lb[7];  // lane (q, m), q = lane / 7: column m of off-diagonal block b0 + 1 + q (rows 0..6)
+  double yv;     // lane < 7: the forward-substituted rhs y_j
+  int xrow;      // that block's row (index into X), -1 when the lane has no block
+};
+
+__device__ __forceinline__ SpBack sp_back_load(const BaArgs& a, const SpTables& T, int j, int lane) {
+  SpBack d;
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int q = lane / 7, m = lane - 7 * (lane / 7);
-  const double* D = a.L + (size_t)b0 * 64;
-  double dl[8][8];  // L_jj (lower) and 1/L_mm (column 7), issued before the sums
+  d.yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
+  const int b = b0 + 1 + q;
+  d.xrow = (lane < 63 && b < b1) ? T.rowL[b] : -1;
+  const double* Lb = a.L + (size_t)(d.xrow >= 0 ? b : b0) * 64 + m;
 #pragma unroll
-  for (int r = 0; r < 7; r++) {
-    double row[8];
-    ld_row(row, D + r * 8);
+  for (int r = 0; r < 7; r++) d.lb[r] = d.xrow >= 0 ? Lb[r * 8] : 0.0;
+  return d;
+}
+
+__device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& T, double* X, int j, const SpBack& d,
+                                               int lane, double* red) {
+  const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
+  const int q = lane / 7, m = lane - 7 * (lane / 7);
+  // lane m < 7: row m of the diagonal block = (L_jj^-1)[i][m] (i > m) | 1/L_mm (column 7), needed last: its load
+  // overlaps the sums (kept out of SpBack for the VGPR budget)
+  double dr[8];
 #pragma unroll
-    for (int c = 0; c < 8; c++) dl[r][c] = row[c];
-  }
-  const double yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
+  for (int c = 0; c < 8; c++) dr[c] = 0.0;
+  if (lane < 7) ld_row(dr, a.L + (size_t)b0 * 64 + lane * 8);
   double acc = 0.0;
-  if (lane < 63)
-    for (int b = b0 + 1 + q; b < b1; b += 9) {
+  if (d.xrow >= 0) {
+    const double* xi = X + (size_t)d.xrow * 8;
+#pragma unroll
+    for (int r = 0; r < 7; r++) acc = fma(d.lb[r], xi[r], acc);
+  }
+  if (lane < 63)  // columns of more than 9 off-diagonal blocks: the rest, loaded here
+    for (int b = b0 + 1 + q + 9; b < b1; b += 9) {
       const double* Lb = a.L + (size_t)b * 64 + m;
       const double* xi = X + (size_t)T.rowL[b] * 8;
 #pragma unroll
@@ -814,26 +850,18 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
   red[lane] = acc;
   wave_sync();
   if (lane < 7) {
-    double sacc = yv;
+    double sacc = d.yv;
 #pragma unroll
     for (int qq = 0; qq < 9; qq++) sacc -= red[qq * 7 + lane];  // fixed order: deterministic
     red[lane] = sacc;
   }
   wave_sync();
-  double z[7];
+  if (lane < 7) {  // x_m = sum_{i >= m} (L_jj^-1)[i][m] z_i: seven independent dot products
+    double x = dr[7] * red[lane];
 #pragma unroll
-  for (int mm = 0; mm < 7; mm++) z[mm] = red[mm];
-  double x[7];
-#pragma unroll
-  for (int mm = 6; mm >= 0; mm--) {
-    double vv = z[mm];
-#pragma unroll
-    for (int p = mm + 1; p < 7; p++) vv = fma(-dl[p][mm], x[p], vv);
-    x[mm] = vv * dl[mm][7];
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int mm = 0; mm < 7; mm++) X[(size_t)j * 8 + mm] = x[mm];
+    for (int i = 1; i < 7; i++)
+      if (i > lane) x = fma(dr[i], red[i], x);
+    X[(size_t)j * 8 + lane] = x;
   }
   wave_sync();
 }
@@ -901,14 +929,40 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     SPST(2 + l);
   }
   // back substitution, levels from the root down; runs of single-column levels stay on wave 0 with no
-  // barrier between them (X in LDS: a wave's LDS accesses are ordered)
-  for (int l = nlev - 1; l >= 0; l--) {
-    const int c0 = T.lev_ptr[l], c1 = T.lev_ptr[l + 1];
-    for (int c = c0 + w; c < c1; c += SP_WAVES) sp_back_column(a, T, X, T.lev_col[c], lane, s_red[w]);
-    const bool chain = LT && c1 - c0 == 1 && l > 0 && T.lev_ptr[l] - T.lev_ptr[l - 1] == 1;
-    if (!chain) {
-      __syncthreads();
-      SPST(3 + nlev + (nlev - 1 - l));
+  // barrier between them (X in LDS: a wave's LDS accesses are ordered). Each wave walks its columns (c0 + w,
+  // c0 + w + 16, ... of every level) in order and loads the next one's factor data ahead (SpBack).
+  {
+    // the wave's next task at or below level l starting from index c (-1: none)
+    auto next_task = [&](int l, int c, int* nl) -> int {
+      for (; l >= 0; l--) {
+        const int lo_c = T.lev_ptr[l], hi_c = T.lev_ptr[l + 1];
+        if (c < 0) c = lo_c + w;
+        if (c < hi_c) {
+          *nl = l;
+          return c;
+        }
+        c = -1;
+      }
+      return -1;
+    };
+    int pl = 0;
+    int pc = next_task(nlev - 1, -1, &pl);
+    SpBack pre = sp_back_load(a, T, pc >= 0 ? T.lev_col[pc] : 0, lane);
+    for (int l = nlev - 1; l >= 0; l--) {
+      const int c0 = T.lev_ptr[l], c1 = T.lev_ptr[l + 1];
+      for (int c = c0 + w; c < c1; c += SP_WAVES) {  // == (pl, pc)
+        const SpBack cur = pre;
+        const int j = T.lev_col[c];
+        int nl = 0;
+        pc = next_task(l, c + SP_WAVES, &nl);
+        if (pc >= 0) pre = sp_back_load(a, T, T.lev_col[pc], lane);  // in flight during this column
+        sp_back_column(a, T, X, j, cur, lane, s_red[w]);
+      }
+      const bool chain = LT && c1 - c0 == 1 && l > 0 && T.lev_ptr[l] - T.lev_ptr[l - 1] == 1;
+      if (!chain) {
+        __syncthreads();
+        SPST(3 + nlev + (nlev - 1 - l));
+      }
     }
   }
   __syncthreads();
