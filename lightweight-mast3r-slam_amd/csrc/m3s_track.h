@@ -56,29 +56,18 @@ struct TrackArgs {
   double* partials;            // (nparts, 40) block partial sums (workspace)
   TrackState* state;
   unsigned long long* cnt;     // (8 x 16) setup counters, one 128-B line per XCD shard: (n_valid_kf << 32) | n_valid_opt
-  unsigned* tick;              // (11 x 32) GN arrival tickets: 8 shards + the top counter, one 128-B line each,
-                               // then the GnBcast record (two lines)
+  unsigned* tick;              // (M3S_TRACK_TICK_WORDS) GN shard tickets, publish ticket, GN shard-sum granules
   float* T_out;                // (16) nullable: T_WCf | T_CkCf written by the solving block when done
   const float* T_WCf;          // (8) the frame's pose estimate (device), read by track_setup's state init
   const float* T_WCk;          // (8) the keyframe's pose (device)
 };
 
-// Per-iteration broadcast of the persistent GN launch, written write-through (sc1) by the block that
-// solved the iteration: 8-byte {data, tag} granules (MI355X_MICROARCH.md, persistent-kernel price list,
-// "Granule"), polled with sc1 loads; old_cost / iter / status are stored before the granules (drained)
-// and read only by the next solving block.
-struct GnBcast {
-  // granules {value bits, generation}: T_CkCf[0..7] and the done flag of the last solved iteration; a
-  // block polls them directly (the tag says the value is the new one: no separate flag round trip)
-  unsigned long long g[9];
-  double old_cost;  // that iteration's cost (the next convergence test's old_cost)
-  int iter;         // iterations done
-  int status;       // M3S_TRACK_*
-  int pad[4];
-};
-// tickets (8 shards + top), the GnBcast record (two lines), the fuse kernel's publish ticket (one line)
-#define M3S_TRACK_TICK_WORDS ((M3S_TRACK_SHARDS + 1 + 2 + 1) * 32)
-#define M3S_TRACK_PUBLISH_TICKET ((M3S_TRACK_SHARDS + 1 + 2) * 32)
+// The tick region (zeroed per frame by track_init): one 128-B line per XCD shard ticket of the persistent GN
+// launch (monotonic within the frame), the fuse kernel's publish ticket (one line), then the shard-sum granules
+// of the GN launch: [2 iteration parities][8 shards][72] 8-byte {32-bit half of a shard sum, iteration + 1}.
+#define M3S_TRACK_PUBLISH_TICKET (M3S_TRACK_SHARDS * 32)
+#define M3S_TRACK_GRANULES ((M3S_TRACK_SHARDS + 1) * 32)
+#define M3S_TRACK_TICK_WORDS (M3S_TRACK_GRANULES + 2 * M3S_TRACK_SHARDS * 72 * 2)
 
 // The frame's result as the host reads it: a copy of the final TrackState in fine-grained (coherent)
 // pinned host memory, written by the fuse launch once n_unique is complete and then released with the

@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) track_init_kernel(uint4* flags, int n16, 
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) flags[i] = make_uint4(0u, 0u, 0u, 0u);
   if (i < M3S_TRACK_SHARDS * 16) cnt[i] = 0ull;
-  for (int j = i; j < M3S_TRACK_TICK_WORDS; j += gridDim.x * blockDim.x) tick[j] = 0u;  // tickets + GnBcast
+  for (int j = i; j < M3S_TRACK_TICK_WORDS; j += gridDim.x * blockDim.x) tick[j] = 0u;  // tickets + granules
 }
 
 // state <- {0, T = T_WCk^-1 * T_WCf (tracker.py:180/225), T_WCk, old_cost = inf}
@@ -292,9 +292,10 @@ __device__ GnStep gn_step(const TrackParams& p, const double* sum, const float* 
 
 #ifdef M3S_GN_STAMPS  // (experiment builds only) s_memrealtime stamps of block 0 / the last block
 __device__ unsigned long long g_gn_stamps[8 * 16];
-#define GN_STAMP(k)                                                                                \
-  do {                                                                                             \
-    if (threadIdx.x == 0 && iter0 < 8) g_gn_stamps[iter0 * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+#define GN_STAMP(k)                                                                                  \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && iter0 < 8 && (blockIdx.x == 0 || (k) == 3 || (k) == 4))                  \
+      g_gn_stamps[iter0 * 16 + (k)] = __builtin_amdgcn_s_memrealtime();                              \
   } while (0)
 #else
 #define GN_STAMP(k) \
@@ -305,35 +306,77 @@ __device__ unsigned long long g_gn_stamps[8 * 16];
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gull;
 
 #define GN_THREADS 256
 #define GN_PPT 4     // points per thread per round: all their record loads issued before any math
-#define GN_LDS_LD 37  // row pitch (doubles) of the transpose buffer: 36 sums + 1 pad
 
-// Deterministic block sum of 36 fp64 values per thread through an LDS transpose: thread t writes
-// its row, then 7 groups x 36 columns of threads sum fixed row subsets, then 36 threads add the 7
-// group sums in order. Replaces 36 six-step shuffle butterflies (measured ~8 us per launch).
-__device__ __forceinline__ void block_sum36(const double* v, double (*s_all)[GN_LDS_LD], double (*s_grp)[GN_NSUM],
-                                            double* out) {
+// ---- the 36 fp64 sums of a wave, reduce-scattered over its lanes (deterministic, no LDS) ----
+// Six half-exchange steps: lanes l and l^32 (v_permlane32_swap: the two halves of a register pair trade places,
+// no selects), l and l^16 (v_permlane16_swap), then within each 16-lane row l^8 (DPP row_ror:8), the 8-lane
+// mirror pairs (row_half_mirror), l^2 and l^1 (quad_perm). At every step a lane keeps one half of its current
+// sums and adds the partner's copy of that half. Afterwards lane gn_lane_of(c) holds the wave's total of sum c
+// (the other 28 lanes hold padding zeros). Fixed order: identical in every block and every run.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
+  int2 x = __builtin_bit_cast(int2, v);
+  switch (ctrl_sel) {  // compile-time after unrolling
+    case 0: x.x = __builtin_amdgcn_mov_dpp(x.x, 0x128, 0xF, 0xF, false); x.y = __builtin_amdgcn_mov_dpp(x.y, 0x128, 0xF, 0xF, false); break;
+    case 1: x.x = __builtin_amdgcn_mov_dpp(x.x, 0x141, 0xF, 0xF, false); x.y = __builtin_amdgcn_mov_dpp(x.y, 0x141, 0xF, 0xF, false); break;
+    case 2: x.x = __builtin_amdgcn_mov_dpp(x.x, 0x4E, 0xF, 0xF, false); x.y = __builtin_amdgcn_mov_dpp(x.y, 0x4E, 0xF, 0xF, false); break;
+    default: x.x = __builtin_amdgcn_mov_dpp(x.x, 0xB1, 0xF, 0xF, false); x.y = __builtin_amdgcn_mov_dpp(x.y, 0xB1, 0xF, 0xF, false); break;
+  }
+  return __builtin_bit_cast(double, x);
+}
+
+// a and b trade their upper-32 / lower-32 lane halves (W = 32) or, within each 32-lane half, their upper-16 /
+// lower-16 quarters (W = 16); returns a' + b': lanes of the lower part hold a + a(partner), the upper part b + b(partner)
+template <int W>
+__device__ __forceinline__ double swap_add(double a, double b) {
+  const int2 xa = __builtin_bit_cast(int2, a), xb = __builtin_bit_cast(int2, b);
+  int2 na, nb;
+  if constexpr (W == 32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(xa.x, xb.x, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(xa.y, xb.y, false, false);
+    na = int2{(int)lo[0], (int)hi[0]};
+    nb = int2{(int)lo[1], (int)hi[1]};
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap(xa.x, xb.x, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(xa.y, xb.y, false, false);
+    na = int2{(int)lo[0], (int)hi[0]};
+    nb = int2{(int)lo[1], (int)hi[1]};
+  }
+  return __builtin_bit_cast(double, na) + __builtin_bit_cast(double, nb);
+}
+
+// one DPP step: n live sums -> ceil(n/2); the lanes with `bit` set keep the upper half
+template <int N, int SEL>
+__device__ __forceinline__ void dpp_step(double* v, bool upper) {
+  constexpr int H = (N + 1) / 2;
 #pragma unroll
-  for (int c = 0; c < GN_NSUM; c++) s_all[threadIdx.x][c] = v[c];
-  __syncthreads();
-  if (threadIdx.x < 7 * GN_NSUM) {
-    const int c = threadIdx.x % GN_NSUM, g = threadIdx.x / GN_NSUM;
-    double a0 = 0.0, a1 = 0.0;
-    int r = g;
-    for (; r + 7 < GN_THREADS; r += 14) {
-      a0 += s_all[r][c];
-      a1 += s_all[r + 7][c];
-    }
-    if (r < GN_THREADS) a0 += s_all[r][c];
-    s_grp[g][c] = a0 + a1;
+  for (int i = 0; i < H; i++) {
+    const double lo = v[i], hi = i + H < N ? v[i + H] : 0.0;
+    const double keep = upper ? hi : lo, give = upper ? lo : hi;
+    v[i] = keep + dpp_f64(give, SEL);
   }
-  __syncthreads();
-  if (threadIdx.x < GN_NSUM) {
-    const int c = threadIdx.x;
-    out[c] = (((((s_grp[0][c] + s_grp[1][c]) + s_grp[2][c]) + s_grp[3][c]) + s_grp[4][c]) + s_grp[5][c]) + s_grp[6][c];
-  }
+}
+
+// lane holding sum c after wave_sum36 (c < 36)
+__device__ __forceinline__ int gn_lane_of(int c) {
+  const int r = c / 9, k = c - 9 * r;  // 16-lane row r, position k of {0,1,2,4,5,8,9,10,12}
+  const int pos = (k < 3) ? k : (k < 5) ? k + 1 : (k < 8) ? k + 3 : 12;
+  return 16 * r + pos;
+}
+
+__device__ __forceinline__ double wave_sum36(double (&v)[GN_NSUM], int lane) {
+#pragma unroll
+  for (int i = 0; i < 18; i++) v[i] = swap_add<32>(v[i], v[i + 18]);
+#pragma unroll
+  for (int i = 0; i < 9; i++) v[i] = swap_add<16>(v[i], v[i + 9]);
+  dpp_step<9, 0>(v, lane & 8);
+  dpp_step<5, 1>(v, lane & 4);
+  dpp_step<3, 2>(v, lane & 2);
+  dpp_step<2, 3>(v, lane & 1);
+  return v[0];
 }
 
 __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, float4 r0, float4 r1, double* acc) {
@@ -394,13 +437,18 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
   }
 }
 
-// All GN iterations in ONE launch (nparts <= 256 blocks, one per CU, so every block is resident). Per
-// iteration: every block accumulates its points' 36 fp64 sums, publishes them write-through and takes an
-// arrival ticket; the last arriver reduces the partials in a fixed order, solves, retracts, tests
-// convergence and broadcasts {T, cost, iter, done} through the GnBcast record; the other blocks poll
-// its generation word and continue with the new T (no kernel boundary, no empty launches after
-// convergence). Spins are bounded: a stalled hand-off ends the solve (status STALLED, which the host reports
-// as an error), never hangs the GPU. The host sizes the grid by the occupancy query (m3s_track_max_parts).
+// All GN iterations in ONE launch (nparts <= 256 blocks, sized by the occupancy query so every block is
+// resident). Per iteration:
+//   1. every block accumulates its points' 36 fp64 sums, reduce-scatters them in each wave (wave_sum36) and
+//      adds the 4 waves' totals in LDS (fixed order), publishes the block partial with write-through (sc1)
+//      stores into the iteration's slot and takes a ticket on its XCD shard (blocks b and b + 8 share one);
+//   2. the shard's last arriver loads its shard's partials with sc1 loads (no acquire fence: every partial byte
+//      was stored sc1 and drained before its ticket, MI355X_MICROARCH.md "Valid forms" row 1), sums them in
+//      block order and publishes the shard sum as 72 tagged 8-byte granules {32-bit half, iteration};
+//   3. every block polls the 8 shard sums (one wave, sc1 loads), adds them in shard order and solves the 7x7
+//      system, retracts and tests convergence itself: the same instructions on the same bytes, so every block
+//      holds the same T bit for bit, and no broadcast hop or serial last-block tail sits on the chain.
+// Spins are bounded: a stalled hand-off ends the frame with status STALLED (the host raises), never a hang.
 __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackParams p) {
   TrackState* st = a.state;
   if (st->done) return;
@@ -416,19 +464,25 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     }
     return;
   }
-  __shared__ double s_all[GN_THREADS][GN_LDS_LD];
-  __shared__ double s_grp[7][GN_NSUM];
+  __shared__ double s_w[GN_THREADS / 64][64];  // per-wave totals (wave_sum36 lanes)
   __shared__ double s_sum[GN_NSUM];
-  __shared__ int s_last;
-  __shared__ int s_stop;
+  __shared__ double s_grp[7][GN_NSUM];
+  __shared__ double s_shard[M3S_TRACK_SHARDS][GN_NSUM];
+  __shared__ int s_last, s_stop, s_fin;
   __shared__ float s_T[8];
-  __shared__ int s_bc[9];
-  GnBcast* bc = reinterpret_cast<GnBcast*>(a.tick + 32 * (M3S_TRACK_SHARDS + 1));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned nblk = gridDim.x;
+  const int shard = blockIdx.x % M3S_TRACK_SHARDS;
+  const int nsh = (int)min(nblk, (unsigned)M3S_TRACK_SHARDS);
+  const unsigned per = (nblk - shard + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;  // blocks in this shard
   float T[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) T[c] = st->T[c];
+  double old = st->old_cost;  // the convergence test's previous cost (inf before the first solve)
+  int iters_done = 0, status = M3S_TRACK_RUNNING;
+  double cost = 0.0;
   const float4* rec = reinterpret_cast<const float4*>(a.rec);
-  const int stride = gridDim.x * GN_THREADS;
+  const int stride = nblk * GN_THREADS;
   // the first round's records (every point at 512x512: 4 per thread) stay in registers for all iterations;
   // only the poses change between iterations
   const int n00 = blockIdx.x * GN_THREADS + threadIdx.x;
@@ -439,11 +493,12 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     c0[u] = rec[2 * (size_t)n];
     c1[u] = rec[2 * (size_t)n + 1];
   }
+  gu32* gran = (gu32*)(a.tick + M3S_TRACK_GRANULES);  // [2 parities][8 shards][72] x {half, tag}
   for (int it = 0; it < p.max_iters; it++) {
 #ifdef M3S_GN_STAMPS
     const int iter0 = it;
 #endif
-    if (blockIdx.x == 0) GN_STAMP(0);
+    GN_STAMP(0);
     double acc[GN_NSUM];
 #pragma unroll
     for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
@@ -462,109 +517,77 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       for (int u = 0; u < GN_PPT; u++)
         if (n0 + u * stride < p.N) gn_point(p, T, r0[u], r1[u], acc);
     }
-    if (blockIdx.x == 0) GN_STAMP(1);
-    block_sum36(acc, s_all, s_grp, s_sum);
+    GN_STAMP(1);
+    s_w[wid][lane] = wave_sum36(acc, lane);
     __syncthreads();
-    if (blockIdx.x == 0) GN_STAMP(2);
-    // publish this block's partial write-through (sc1 agent-scope stores) into the iteration's own slot (a
-    // slot no L2 has seen in this launch), drain, take a ticket
-    const int slot = it < GN_SLOTS ? it : GN_SLOTS - 1;
+    // the block partial: 36 threads add the 4 waves' totals, store it write-through into this iteration's slot
+    const int slot = it % GN_SLOTS;
     gdouble* part = (gdouble*)(a.partials + (size_t)slot * GN_THREADS * GN_PSTRIDE);
-    if (threadIdx.x < GN_NSUM)
-      __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
+    if (threadIdx.x < GN_NSUM) {
+      const int l = gn_lane_of(threadIdx.x);
+      const double v = ((s_w[0][l] + s_w[1][l]) + s_w[2][l]) + s_w[3][l];
+      __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {  // two-level ticket: this block's XCD shard, then the top counter by each shard's last
-      const unsigned sh = blockIdx.x % M3S_TRACK_SHARDS;
-      const unsigned nsh = min(gridDim.x, (unsigned)M3S_TRACK_SHARDS);
-      const unsigned per = (gridDim.x - sh + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;
-      bool last = false;
-      if (__hip_atomic_fetch_add((gu32*)&a.tick[32 * sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1)
-        last = __hip_atomic_fetch_add((gu32*)&a.tick[32 * M3S_TRACK_SHARDS], 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
-      s_last = last;
+    GN_STAMP(2);
+    if (threadIdx.x == 0) {  // the shard ticket (monotonic within the frame: it + 1 rounds of `per` arrivals)
+      const unsigned t = __hip_atomic_fetch_add((gu32*)&a.tick[32 * shard], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      s_last = t == (unsigned)(it + 1) * per - 1;
       s_stop = 0;
     }
     __syncthreads();
+    const int par = it & 1;
     if (s_last) {
       GN_STAMP(3);
-      // last arriver: acquire (invalidates this CU's L1); thread (c, g) sums column c of the partial rows g,
-      // g + 7, ... straight from this iteration's slot (no L2 has held it in this launch), all 37 loads in
-      // flight at once: the same fixed order as block_sum36 (whose rows beyond the grid are zeros), without its
-      // LDS transpose. Past GN_SLOTS - 1 iterations the last slot is reused and read with sc1 loads.
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      static_assert(GN_THREADS == 256, "the unrolled column walk below assumes 256 partial rows");
+      // the shard's partial rows (blocks shard, shard + 8, ...), thread (c, g) walks column c over rows g, g + 7,
+      // ... with sc1 loads, then the 7 group sums in order
       if (threadIdx.x < 7 * GN_NSUM) {
         const int c = threadIdx.x % GN_NSUM, g = threadIdx.x / GN_NSUM;
-        const int nrow = (int)gridDim.x;
-        const bool fresh = it < GN_SLOTS - 1;
-        const gdouble* col = part + c;
-        auto ld = [&](int r) -> double {
-          if (r >= nrow) return 0.0;
-          return fresh ? col[(size_t)r * GN_PSTRIDE]
-                       : __hip_atomic_load(&col[(size_t)r * GN_PSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-        for (int k = 0; k < 18; k++) {  // rows g + 14k (a0) and g + 14k + 7 (a1), all < 256
-          a0 += ld(g + 14 * k);
-          a1 += ld(g + 14 * k + 7);
-        }
-        if (g < 4) a0 += ld(g + 252);
-        s_grp[g][c] = a0 + a1;
+        double s0 = 0.0;
+        for (unsigned r = g; r < per; r += 7)
+          s0 += __hip_atomic_load(&part[(size_t)(shard + 8 * r) * GN_PSTRIDE + c], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        s_grp[g][c] = s0;
       }
       __syncthreads();
-      if (threadIdx.x < GN_NSUM) {
-        const int c = threadIdx.x;
-        s_sum[c] = (((((s_grp[0][c] + s_grp[1][c]) + s_grp[2][c]) + s_grp[3][c]) + s_grp[4][c]) + s_grp[5][c]) +
-                   s_grp[6][c];
+      if (threadIdx.x < 2 * GN_NSUM) {  // 72 granules: the lower / upper 32 bits of each shard sum, tagged it + 1
+        const int c = threadIdx.x >> 1;
+        const double v = (((((s_grp[0][c] + s_grp[1][c]) + s_grp[2][c]) + s_grp[3][c]) + s_grp[4][c]) + s_grp[5][c]) +
+                         s_grp[6][c];
+        const unsigned long long bits = __builtin_bit_cast(unsigned long long, v);
+        const unsigned half = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+        __hip_atomic_store((gull*)&gran[2 * ((par * M3S_TRACK_SHARDS + shard) * 2 * GN_NSUM + threadIdx.x)],
+                           ((unsigned long long)(it + 1) << 32) | half, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __syncthreads();
       GN_STAMP(4);
-      if (threadIdx.x == 0) {
-        // the previous iteration's cost (the convergence test's old_cost): from the state before the
-        // first solve, from the broadcast record after it
-        const double old = it == 0 ? st->old_cost : __hip_atomic_load(&bc->old_cost, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT);
-        const GnStep r = gn_step(p, s_sum, T, it, old);
-        __hip_atomic_store(&bc->old_cost, r.cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&bc->iter, r.iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&bc->status, r.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_bc[8] = r.done;
-        for (int c = 0; c < 8; c++) s_T[c] = r.T[c];
-#ifdef M3S_GN_STAMPS
-        if (iter0 < 8) g_gn_stamps[iter0 * 16 + 5] = __builtin_amdgcn_s_memrealtime();
-#endif
-      }
-      if (threadIdx.x <= M3S_TRACK_SHARDS)  // every block has arrived: re-arm the tickets for the next iteration
-        __hip_atomic_store((gu32*)&a.tick[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x < 9) {  // the granules, after everything above has drained
-        const unsigned val = threadIdx.x < 8 ? __float_as_uint(s_T[threadIdx.x]) : (unsigned)s_bc[8];
-        __hip_atomic_store(&bc->g[threadIdx.x], ((unsigned long long)(it + 1) << 32) | val, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (threadIdx.x < 64) {
-      // wave 0 polls the 9 granules (one lane each) until every tag is this iteration's
+    }
+    if (threadIdx.x < 64) {
+      // wave 0 polls every shard's 72 granules (lane l: granules l, l + 64, ... of the nsh x 72), until every tag
+      // is this iteration's
+      const int ng = nsh * 2 * GN_NSUM;
       unsigned spins = 0;
-      unsigned long long gv = 0;
       for (;;) {
         bool ok = true;
-        if (threadIdx.x < 9) {
-          gv = __hip_atomic_load(&bc->g[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = (unsigned)(gv >> 32) == (unsigned)(it + 1);
+        for (int g = lane; g < ng; g += 64) {
+          const unsigned long long v = __hip_atomic_load(
+              (gull*)&gran[2 * (par * M3S_TRACK_SHARDS * 2 * GN_NSUM + g)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(v >> 32) != (unsigned)(it + 1)) {
+            ok = false;
+          } else {
+            unsigned* w = reinterpret_cast<unsigned*>(&s_shard[0][0]);
+            w[g] = (unsigned)v;  // lo/hi words in place: granule g = shard g / 72, sum (g % 72) / 2, half g % 2
+          }
         }
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 23)) {  // a lost hand-off (~0.25 s): stop with status STALLED (the host raises)
-          if (threadIdx.x == 0) s_stop = 1;
+        if (++spins > (1u << 22)) {  // a lost hand-off (~0.25 s): stop with status STALLED (the host raises)
+          if (lane == 0) s_stop = 1;
           break;
         }
       }
-      if (threadIdx.x < 8) s_T[threadIdx.x] = __uint_as_float((unsigned)gv);
-      if (threadIdx.x == 8) s_bc[8] = (int)(unsigned)gv;
     }
     __syncthreads();
     if (s_stop) {
@@ -574,18 +597,35 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       }
       return;
     }
+    GN_STAMP(5);
+    if (threadIdx.x < GN_NSUM) {  // the frame's sums: the shard sums in shard order
+      const int c = threadIdx.x;
+      double v = s_shard[0][c];
+      for (int k = 1; k < nsh; k++) v += s_shard[k][c];
+      s_sum[c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const GnStep r = gn_step(p, s_sum, T, it, old);
+      for (int c = 0; c < 8; c++) s_T[c] = r.T[c];
+      s_fin = r.done;
+      old = r.cost;
+      cost = r.cost;
+      iters_done = r.iter;
+      status = r.status;
+    }
+    __syncthreads();
+    GN_STAMP(6);
 #pragma unroll
     for (int c = 0; c < 8; c++) T[c] = s_T[c];
-    const bool fin = s_bc[8] != 0;
-    __syncthreads();  // s_T / s_bc are rewritten in the next iteration
+    const bool fin = s_fin != 0;
+    __syncthreads();  // s_T / s_fin are rewritten in the next iteration
     if (fin) break;
   }
-  // the final state, written by ONE block (plain stores of a single writer; the host and the fuse launch
-  // read it after this launch)
+  // the final state, written by ONE block (plain stores of a single writer; the host and the fuse launch read it
+  // after this launch); every block holds the same values
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const int status = __hip_atomic_load(&bc->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double cost = __hip_atomic_load(&bc->old_cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st->iter = __hip_atomic_load(&bc->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->iter = iters_done;
     st->last_cost = cost;
     st->old_cost = cost;
     st->status = status;

@@ -33,7 +33,8 @@ torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 128)()
 lib.m3s_debug_gn_stamps(buf)
 print("iters", tracker.last_result.iters, "(stamps in us from block-0 start; 100 MHz clock)")
-names = ["b0 start", "b0 loop done", "b0 reduced", "last: ticket", "last: tail loaded", "last: finish done"]
+names = ["b0 start", "b0 points done", "b0 partial stored", "shard-last start", "shard sum published",
+         "b0 shard sums polled", "b0 solved"]
 for it in range(tracker.last_result.iters):
     t0 = buf[it * 16]
     nxt = f"  next b0 start={(buf[(it + 1) * 16] - t0) / 100:.2f}" if it + 1 < tracker.last_result.iters else ""

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 120 ./scripts/micro/fma_rates > gpurun_out/fma_rates.txt 2>&1
+[ -n "$SKIP_FMA" ] || timeout -k 10 120 ./scripts/micro/fma_rates > gpurun_out/fma_rates.txt 2>&1
 rc=$?; echo "FMA_RATES_RC=$rc"; cat gpurun_out/fma_rates.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -m pytest tests/test_gpu_tracking.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/track_tests.log 2>&1
 rc=$?; echo "TRACK_TESTS_RC=$rc"; tail -3 gpurun_out/track_tests.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
