@@ -557,9 +557,14 @@ __device__ unsigned long long g_sp_stamps[4096];
   do {                                                                                        \
     if (threadIdx.x == 0 && (k) < 3000) g_sp_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// FST(k): phase k of ONE task (column a.nb - 2's factor task, FSTJ = that column), every load of the
+// wave drained first so the stamp falls after the data arrived
 #define FST(k)                                                                              \
   do {                                                                                      \
-    if (lane == 0) g_sp_stamps[3000 + (k)] = __builtin_amdgcn_s_memrealtime();            \
+    if (fst_on) {                                                                           \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                          \
+      if (lane == 0) g_sp_stamps[3000 + (k)] = __builtin_amdgcn_s_memrealtime();          \
+    }                                                                                       \
   } while (0)
 #else
 #define SPST(k) \
@@ -729,13 +734,19 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int noff = b1 - b0 - 1, nrow = 7 * (noff + 1) + 1;
   const bool has1 = lane < nrow, has2 = lane + 64 < nrow;
+#ifdef M3S_SP_STAMPS
+  const bool fst_on = j == a.nb - 2;
+#endif
+  FST(0);
   double v1[8], v2[8];
   double* p1 = has1 ? sp_row_addr(a, b0, noff, j, lane) : nullptr;
   double* p2 = has2 ? sp_row_addr(a, b0, noff, j, lane + 64) : nullptr;
   if (has1) ld_row(v1, p1);
   if (has2) ld_row(v2, p2);
+  FST(1);
   const int g = T.pull_grp[j];
   if (g >= 0) sp_group_regs(a, T, g, noff, nrow, v1, v2, lane, bjk);
+  FST(2);
   bool fail = false;
   double inv[7], lo[21];
 #pragma unroll
@@ -778,9 +789,17 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
     for (int m = 1; m < 7; m++) iv = lane == m ? inv[m] : iv;
     v1[7] = iv;
   }
+  FST(3);
   if (has1) st_row(p1, v1);
   if (has2) st_row(p2, v2);
   if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, g, lo, inv, lane, bjk);
+  FST(4);
+#ifdef M3S_SP_STAMPS
+  if (fst_on && lane == 0) {
+    g_sp_stamps[3010] = noff;
+    g_sp_stamps[3011] = g >= 0 ? T.grp[g].z - T.grp[g].y : 0;
+  }
+#endif
 }
 
 // B. update group g (one wave): the rows of its target column take the group's sources, loaded and

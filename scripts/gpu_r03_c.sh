@@ -18,3 +18,5 @@ for k in ('ba',):
     c=b['c4']; print('C4', {x: c[x] for x in ('edges_per_s','ms_per_call','ms_setup','ms_lin_per_iter','ms_solve_per_iter')}, c['roofline']['frac'])
 "; [ $rc -eq 0 ] || { tail -30 gpurun_out/bench.err; exit $rc; }
 bash scripts/gpu_r03_b.sh
+M3S_LIB=lightweight-mast3r-slam_amd/lib/exp/libm3s_spst.so timeout -k 10 200 python3 scripts/ba_exp.py 256 384 512 3 chess calib > gpurun_out/sp_stamps.txt 2>&1
+echo "SP_STAMPS_RC=$?"; tail -5 gpurun_out/sp_stamps.txt
