@@ -643,7 +643,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   }
   // the leaf end of the elimination tree runs as multi-workgroup launches (steps [0, wide_steps)), the root end
   // in the one-workgroup kernel. The split minimises the measured step costs (MI355X, C5/C4 graphs): a launch
-  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of 16 waves (one wave per task).
+  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of M3S_BA_SP_WAVES waves (one wave per task).
   // M3S_BA_WIDE=t (tests, experiments): every step up to the last one with more than t tasks instead.
   std::vector<int> tasks(S.nlev + 1);
   for (int l = 0; l <= S.nlev; l++) {
@@ -661,7 +661,8 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   } else {
     constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
     std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
-    for (int l = lmax - 1; l >= 0; l--) suffix[l] = suffix[l + 1] + kRoundUs * ((tasks[l] + 15) / 16);
+    for (int l = lmax - 1; l >= 0; l--)
+      suffix[l] = suffix[l + 1] + kRoundUs * ((tasks[l] + M3S_BA_SP_WAVES - 1) / M3S_BA_SP_WAVES);
     int best_L = 0;
     double best = suffix[0];
     for (int L = 1; L <= lmax; L++) {

@@ -514,7 +514,8 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL) {
   *out = s;
 }
 
-constexpr int SP_WAVES = 16;                 // waves of the factor workgroup
+constexpr int SP_WAVES = M3S_BA_SP_WAVES;    // waves of the factor workgroup (256-VGPR budget at 8 waves)
+constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_PLAN_BYTES = 144 * 1024;   // LDS for the plan's loop tables and the solution x
 
 // 1/sqrt(d) for d > 0: the v_rsq_f64 estimate (~2^-22 relative) refined by ONE Newton step (~2^-44)
@@ -747,26 +748,54 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
   const int g = T.pull_grp[j];
   if (g >= 0) sp_group_regs(a, T, g, noff, nrow, v1, v2, lane, bjk);
   FST(2);
+  // the 7x7 diagonal block: its rows (lanes 0..6) go through LDS and EVERY lane factors it redundantly in
+  // registers (left-looking; no cross-lane broadcasts on the pivot chain), then each lane solves its own rows
+  // x L_jj^T = a (the off-diagonal rows give L_ij, the rhs row the forward substitution y_j = L_jj^-1 b_j)
+  if (lane < 7) {
+#pragma unroll
+    for (int c = 0; c < 7; c++)
+      if (c <= lane) bjk[lane * 7 + c] = v1[c];
+  }
+  wave_sync();
   bool fail = false;
-  double inv[7], lo[21];
+  double inv[7], lo[21], ldg[7];  // lo[r (r - 1) / 2 + c] = L[r][c] (c < r), ldg[m] = L[m][m]
 #pragma unroll
   for (int m = 0; m < 7; m++) {
-    double d = bcast_lane(v1[m], m);
+    double d = bjk[m * 7 + m];
+#pragma unroll
+    for (int k = 0; k < m; k++) d = fma(-lo[m * (m - 1) / 2 + k], lo[m * (m - 1) / 2 + k], d);
     if (!(d > 0.0)) {  // not positive definite: the step is discarded (dx = 0), as SimplicialLLT's info
       fail = true;
       d = 1.0;
     }
     inv[m] = rsqrt_nr(d);
-    const double l1 = v1[m] * inv[m], l2 = v2[m] * inv[m];
-    v1[m] = lane == m ? d * inv[m] : l1;
-    v2[m] = l2;
+    ldg[m] = d * inv[m];
 #pragma unroll
-    for (int c = m + 1; c < 7; c++) {
-      const double lc = bcast_lane(l1, c);
-      lo[c * (c - 1) / 2 + m] = lc;
-      v1[c] = fma(-l1, lc, v1[c]);
-      v2[c] = fma(-l2, lc, v2[c]);
+    for (int r = m + 1; r < 7; r++) {
+      double t = bjk[r * 7 + m];
+#pragma unroll
+      for (int k = 0; k < m; k++) t = fma(-lo[r * (r - 1) / 2 + k], lo[m * (m - 1) / 2 + k], t);
+      lo[r * (r - 1) / 2 + m] = t * inv[m];
     }
+  }
+  wave_sync();  // bjk is free again
+  // own rows: the diagonal rows take L (lower), every other row solves x L^T = a (in order m = 0..6)
+#pragma unroll
+  for (int m = 0; m < 7; m++) {
+    double t1 = v1[m], t2 = v2[m];
+#pragma unroll
+    for (int k = 0; k < m; k++) {
+      t1 = fma(-v1[k], lo[m * (m - 1) / 2 + k], t1);
+      t2 = fma(-v2[k], lo[m * (m - 1) / 2 + k], t2);
+    }
+    v1[m] = t1 * inv[m];
+    v2[m] = t2 * inv[m];
+  }
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+#pragma unroll
+    for (int c = 0; c < r; c++) v1[c] = lane == r ? lo[r * (r - 1) / 2 + c] : v1[c];
+    v1[r] = lane == r ? ldg[r] : v1[r];
   }
   if (fail && lane == 0) *bad = 1;
   if (lane < 7) {
@@ -825,6 +854,7 @@ __device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables&
 // substitution starts, so a wave loads its NEXT column's data (SpBack) while it solves the current one: only
 // the x_i of the ancestors (LDS) sit on the level-to-level chain.
 struct SpBack {
+  double dr[8];  // lane m < 7: row m of the diagonal block = (L_jj^-1)[i][m] (i > m) | 1/L_mm (column 7)
   double lb[7];  // lane (q, m), q = lane / 7: column m of off-diagonal block b0 + 1 + q (rows 0..6)
   double yv;     // lane < 7: the forward-substituted rhs y_j
   int xrow;      // that block's row (index into X), -1 when the lane has no block
@@ -834,6 +864,9 @@ __device__ __forceinline__ SpBack sp_back_load(const BaArgs& a, const SpTables& 
   SpBack d;
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int q = lane / 7, m = lane - 7 * (lane / 7);
+#pragma unroll
+  for (int c = 0; c < 8; c++) d.dr[c] = 0.0;
+  if (lane < 7) ld_row(d.dr, a.L + (size_t)b0 * 64 + lane * 8);
   d.yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
   const int b = b0 + 1 + q;
   d.xrow = (lane < 63 && b < b1) ? T.rowL[b] : -1;
@@ -847,12 +880,6 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
                                                int lane, double* red) {
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int q = lane / 7, m = lane - 7 * (lane / 7);
-  // lane m < 7: row m of the diagonal block = (L_jj^-1)[i][m] (i > m) | 1/L_mm (column 7), needed last: its load
-  // overlaps the sums (kept out of SpBack for the VGPR budget)
-  double dr[8];
-#pragma unroll
-  for (int c = 0; c < 8; c++) dr[c] = 0.0;
-  if (lane < 7) ld_row(dr, a.L + (size_t)b0 * 64 + lane * 8);
   double acc = 0.0;
   if (d.xrow >= 0) {
     const double* xi = X + (size_t)d.xrow * 8;
@@ -876,10 +903,10 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
   }
   wave_sync();
   if (lane < 7) {  // x_m = sum_{i >= m} (L_jj^-1)[i][m] z_i: seven independent dot products
-    double x = dr[7] * red[lane];
+    double x = d.dr[7] * red[lane];
 #pragma unroll
     for (int i = 1; i < 7; i++)
-      if (i > lane) x = fma(dr[i], red[i], x);
+      if (i > lane) x = fma(d.dr[i], red[i], x);
     X[(size_t)j * 8 + lane] = x;
   }
   wave_sync();
@@ -903,7 +930,7 @@ __global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int l) {
 }
 
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
-__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
+__global__ void __launch_bounds__(SP_THREADS) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
   __shared__ __attribute__((aligned(16))) int s_plan[LT ? SP_PLAN_BYTES / 4 : 4];
   __shared__ double s_red[SP_WAVES][64];  // per-wave staging: L_jk and the back-substitution sums
@@ -918,12 +945,12 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     int4* dst = reinterpret_cast<int4*>(s_plan);
     const int n16 = (a.plan_bytes + 15) / 16;
     int4 tmp[8];
-    for (int i0 = 0; i0 < n16; i0 += 8 * 1024) {
+    for (int i0 = 0; i0 < n16; i0 += 8 * SP_THREADS) {
 #pragma unroll
-      for (int u = 0; u < 8; u++) tmp[u] = src[min(i0 + u * 1024 + (int)threadIdx.x, n16 - 1)];
+      for (int u = 0; u < 8; u++) tmp[u] = src[min(i0 + u * SP_THREADS + (int)threadIdx.x, n16 - 1)];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * 1024 + (int)threadIdx.x;
+        const int i = i0 + u * SP_THREADS + (int)threadIdx.x;
         if (i < n16) dst[i] = tmp[u];
       }
     }
@@ -989,14 +1016,14 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   const bool failed = s_bad != 0 || (a.wide_steps > 0 && *a.bad != 0);
   const int n = a.nb * 7;
   float n2 = 0.0f;
-  for (int i = threadIdx.x; i < n; i += 1024) {
+  for (int i = threadIdx.x; i < n; i += SP_THREADS) {
     const int j = i / 7, m = i - 7 * (i / 7);
     const float d = failed ? 0.0f : (float)(-X[(size_t)j * 8 + m]);
     a.dx[a.perm[j] * 7 + m] = d;
     n2 += d * d;
   }
   __syncthreads();
-  for (int k = 1 + threadIdx.x; k < K; k += 1024) {
+  for (int k = 1 + threadIdx.x; k < K; k += SP_THREADS) {
     float Tw[8], xi[7];
     for (int c = 0; c < 8; c++) Tw[c] = a.Twc[k * 8 + c];
     for (int c = 0; c < 7; c++) xi[c] = a.dx[(k - 1) * 7 + c];
@@ -1059,8 +1086,8 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
   for (int l = 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0) hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, l);
   if (((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 <= (size_t)m3s::SP_PLAN_BYTES)
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(m3s::SP_THREADS), 0, s, *a, K, nL, delta_thresh);
   else
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(m3s::SP_THREADS), 0, s, *a, K, nL, delta_thresh);
   return hipGetLastError();
 }

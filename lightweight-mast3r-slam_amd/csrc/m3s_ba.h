@@ -7,6 +7,10 @@
 #define BA_MODE_RAYS 1
 #define BA_MODE_CALIB 2
 
+#ifndef M3S_BA_SP_WAVES
+#define M3S_BA_SP_WAVES 8  // waves of the one-workgroup sparse factorisation (ba.hip) and of its cost model (abi.cpp)
+#endif
+
 struct BaParams {
   int mode;
   int N;            // points per keyframe
