@@ -301,6 +301,10 @@ static int wait_published(const TrackMirror* m, unsigned gen, hipStream_t s) {
   }
 }
 
+// workspaces whose frame scratch the last fuse launch cleared: workspace -> clean byte-map entries (uint4)
+static std::mutex g_track_clean_mu;
+static std::map<const void*, int> g_track_clean;
+
 static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
 
 static size_t track_carve(Carver& c, int N, TrackState** st, uint8_t** flags, double** partials, float** rec,
@@ -407,7 +411,20 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     fa.Nk_new = fuse->Nk_new;
     fa.Nf = fuse->Nf;
   }
-  HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
+  // the previous frame's fuse launch left this workspace's scratch clean (byte map of n16 entries, counters,
+  // tickets): track_init runs only for a fresh / grown / failed workspace
+  const int n16 = (N + 15) / 16;
+  int clean = 0;
+  {
+    std::lock_guard<std::mutex> lock(g_track_clean_mu);
+    auto it = g_track_clean.find(workspace);
+    if (it != g_track_clean.end()) clean = it->second;
+    g_track_clean.erase(workspace);  // dirty until this call has published
+  }
+  if (clean < n16) {
+    HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
+    clean = n16;
+  }
   {
     Span sp("track_setup", s);
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
@@ -428,6 +445,10 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   // blocks may still be running: later work on this stream is ordered after them).
   HIP_TRY(m3s_launch_fuse(&a, 0, &fa, p.direct ? 0 : 1, N, &pub, s), "track fuse launch");
   if (int rc = wait_published(mirror, pub.gen, s)) return rc;
+  {
+    std::lock_guard<std::mutex> lock(g_track_clean_mu);
+    g_track_clean[workspace] = clean;  // the fuse launch cleared what this frame dirtied
+  }
   const TrackState& hs = mirror->s;
   if (hs.status == M3S_TRACK_STALLED)
     return fail(M3S_EHIP, "track: the persistent GN launch's hand-off stalled (its blocks were not co-resident); "

@@ -290,12 +290,13 @@ __device__ GnStep gn_step(const TrackParams& p, const double* sum, const float* 
   return r;
 }
 
-#ifdef M3S_GN_STAMPS  // (experiment builds only) s_memrealtime stamps of block 0 / the last block
-__device__ unsigned long long g_gn_stamps[8 * 16];
+#ifdef M3S_GN_STAMPS  // (experiment builds only) s_memrealtime stamps of every block: [iteration][block][phase]
+#define GN_NSTAMP (8 * 256 * 8)
+__device__ unsigned long long g_gn_stamps[GN_NSTAMP];
 #define GN_STAMP(k)                                                                                  \
   do {                                                                                               \
-    if (threadIdx.x == 0 && iter0 < 8 && (blockIdx.x == 0 || (k) == 3 || (k) == 4))                  \
-      g_gn_stamps[iter0 * 16 + (k)] = __builtin_amdgcn_s_memrealtime();                              \
+    if (threadIdx.x == 0 && iter0 < 8 && blockIdx.x < 256)                                           \
+      g_gn_stamps[(iter0 * 256 + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 #else
 #define GN_STAMP(k) \
@@ -544,13 +545,17 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       GN_STAMP(3);
       // the shard's partial rows (blocks shard, shard + 8, ...), thread (c, g) walks column c over rows g, g + 7,
       // ... with sc1 loads, then the 7 group sums in order
-      if (threadIdx.x < 7 * GN_NSUM) {
+      if (threadIdx.x < 7 * GN_NSUM) {  // <= 32 rows per shard: at most 5 per thread, all loads in flight at once
         const int c = threadIdx.x % GN_NSUM, g = threadIdx.x / GN_NSUM;
-        double s0 = 0.0;
-        for (unsigned r = g; r < per; r += 7)
-          s0 += __hip_atomic_load(&part[(size_t)(shard + 8 * r) * GN_PSTRIDE + c], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        s_grp[g][c] = s0;
+        double v[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+          const unsigned r = g + 7 * k;
+          v[k] = r < per ? __hip_atomic_load(&part[(size_t)(shard + 8 * r) * GN_PSTRIDE + c], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                         : 0.0;
+        }
+        s_grp[g][c] = (((v[0] + v[1]) + v[2]) + v[3]) + v[4];
       }
       __syncthreads();
       if (threadIdx.x < 2 * GN_NSUM) {  // 72 granules: the lower / upper 32 bits of each shard sum, tagged it + 1
@@ -661,31 +666,42 @@ __device__ void publish_state(const TrackState* st, TrackPublish pub) {
   v.n_unique = __hip_atomic_load(&const_cast<TrackState*>(st)->n_unique, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   pub.mirror->s = v;
   __hip_atomic_store(&pub.mirror->gen, pub.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pub.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every counting block arrived
 }
 
+// The counting blocks also leave the frame's scratch clean for the next frame on this workspace (the host then
+// skips track_init): the unique-idx byte map (each entry zeroed by the thread that counted it), the setup
+// counters, the GN shard tickets and granules (the publish ticket is re-armed by its last arriver).
 __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id, FuseArgs f,
-                                                   int N, const uint8_t* __restrict__ flags, int* __restrict__ n_unique,
-                                                   TrackPublish pub) {
+                                                   int N, uint8_t* __restrict__ flags, int* __restrict__ n_unique,
+                                                   TrackPublish pub, int clean_map, unsigned* __restrict__ tick,
+                                                   unsigned long long* __restrict__ cnt_words) {
   const bool solved = st->done && st->done_chunk == chunk_id;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x < FUSE_COUNT_BLOCKS) {
-    if (solved && n_unique != nullptr) {
+    const int tcb = blockIdx.x * 256 + threadIdx.x;  // thread among the counting blocks
+    for (int j = tcb; j < M3S_TRACK_TICK_WORDS; j += FUSE_COUNT_BLOCKS * 256)
+      if (j < M3S_TRACK_PUBLISH_TICKET || j >= M3S_TRACK_GRANULES) tick[j] = 0u;
+    if (tcb < M3S_TRACK_SHARDS * 16) cnt_words[tcb] = 0ull;
+    const bool count = solved && n_unique != nullptr;
+    if (count || clean_map) {
       // |unique(idx[valid])| (tracker.py:106-108): popcount of the byte map track_setup wrote (0/1 bytes,
       // 16-B padded), here after the solve instead of on the first GN iteration's critical path. A few
       // blocks reduce in LDS and add once each: one device-scope atomic per block, not per wave.
       __shared__ int s_cnt[4];
-      const uint4* fl = reinterpret_cast<const uint4*>(flags);
+      uint4* fl = reinterpret_cast<uint4*>(flags);
       const int n16 = (N + 15) / 16;
       int cnt = 0;
-      for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += FUSE_COUNT_BLOCKS * 256) {
+      for (int i = tcb; i < n16; i += FUSE_COUNT_BLOCKS * 256) {
         const uint4 v = fl[i];
         cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        if (clean_map) fl[i] = make_uint4(0u, 0u, 0u, 0u);
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
       if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (threadIdx.x == 0 && count) {
         const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
         if (tot) atomicAdd(n_unique, tot);
       }
@@ -753,7 +769,7 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
                                              int chunk_id, hipStream_t s) {
   (void)iters;
   (void)chunk_id;
-  if (nparts < 1 || nparts > GN_THREADS) return hipErrorInvalidValue;  // the tail loads one partial per thread
+  if (nparts < 1 || nparts > 256) return hipErrorInvalidValue;  // <= 32 blocks per XCD shard (the shard-last loads)
   hipLaunchKernelGGL(m3s::gn_loop_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
   return hipGetLastError();
 }
@@ -763,14 +779,18 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
 extern "C" hipError_t m3s_launch_fuse(const TrackArgs* a, int chunk_id, const FuseArgs* f, int count, int N,
                                       const TrackPublish* pub, hipStream_t s) {
   const int grid = (N + 255) / 256 > FUSE_COUNT_BLOCKS ? (N + 255) / 256 : FUSE_COUNT_BLOCKS;  // every counting block publishes
+  // count: the byte map was written by track_setup (fused path), so it is counted and cleared
   hipLaunchKernelGGL(m3s::fuse_kernel, dim3(grid), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
-                     count ? &a->state->n_unique : nullptr, *pub);
+                     count ? &a->state->n_unique : nullptr, *pub, count, a->tick, a->cnt);
   return hipGetLastError();
 }
 
 #ifdef M3S_GN_STAMPS
 extern "C" int m3s_debug_gn_stamps(unsigned long long* out) {
   (void)hipDeviceSynchronize();
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_gn_stamps), sizeof(unsigned long long) * 128) == hipSuccess ? 0 : -1;
+  const int rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_gn_stamps), sizeof(unsigned long long) * GN_NSTAMP) == hipSuccess ? 0 : -1;
+  static unsigned long long z[GN_NSTAMP];  // zeros: cleared for the next frame (shard-last stamps are sparse)
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(m3s::g_gn_stamps), z, sizeof(z));
+  return rc;
 }
 #endif

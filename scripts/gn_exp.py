@@ -30,12 +30,26 @@ lib = _lib.load()
 for i in range(6):
     tracker.track(Frame(i, (H, W), T_WC=Sim3(kf.T_WC.data.clone())))
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * 128)()
+import numpy as np  # noqa: E402
+
+NB = 8 * 256 * 8
+buf = (ctypes.c_ulonglong * NB)()
+lib.m3s_debug_gn_stamps(buf)  # read + clear the warm-up frames' stamps
+tracker.track(Frame(6, (H, W), T_WC=Sim3(kf.T_WC.data.clone())))
+torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * NB)()
 lib.m3s_debug_gn_stamps(buf)
-print("iters", tracker.last_result.iters, "(stamps in us from block-0 start; 100 MHz clock)")
-names = ["b0 start", "b0 points done", "b0 partial stored", "shard-last start", "shard sum published",
-         "b0 shard sums polled", "b0 solved"]
-for it in range(tracker.last_result.iters):
-    t0 = buf[it * 16]
-    nxt = f"  next b0 start={(buf[(it + 1) * 16] - t0) / 100:.2f}" if it + 1 < tracker.last_result.iters else ""
-    print(f"iter {it}: " + "  ".join(f"{n}={(buf[it * 16 + k] - t0) / 100:.2f}" for k, n in enumerate(names)) + nxt)
+st = np.frombuffer(buf, dtype=np.uint64).reshape(8, 256, 8).astype(np.float64)
+iters = tracker.last_result.iters
+print("iters", iters, "- per-block s_memrealtime stamps (100 MHz), us from the iteration's earliest block start:")
+names = ["start", "points done", "partial stored", "shard-last start", "shard sum published", "shard sums polled",
+         "solved"]
+for it in range(iters):
+    t0 = st[it, :, 0][st[it, :, 0] > 0].min()
+    parts = []
+    for k, n in enumerate(names):
+        v = st[it, :, k]
+        v = v[v > 0]
+        if v.size:
+            parts.append(f"{n} {(v.min() - t0) / 100:.2f}..{(v.max() - t0) / 100:.2f}")
+    print(f"iter {it}: " + " | ".join(parts))
