@@ -164,30 +164,49 @@ __device__ __forceinline__ void pair_flush_v(double* acc, f2* fv, bool odd) {
 //   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
 template <int MODE>
+__device__ __forceinline__ float4 ba_pack_point(const BaArgs& a, const BaParams& p, int ix, int jx, bool vm,
+                                               int64_t ind, float q, float cj) {
+  ind = vm ? ind : 0;
+  const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
+  const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) && (cj > p.C_thresh);
+  // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
+  const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
+  if constexpr (MODE == BA_MODE_CALIB) {
+    const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
+    const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
+    return make_float4((float)u_t, (float)v_t, Xi[2], sw);
+  } else {
+    return make_float4(Xi[0], Xi[1], Xi[2], sw);
+  }
+}
+
+// VEC: 4 consecutive points per thread (N % 4 == 0): the per-point streams (valid, idx, Q, C_j) are read as 4-, 32-,
+// 16- and 16-byte vectors and the records written as four 16-byte stores, instead of one small access per point
+template <int MODE, bool VEC>
 __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int E_local) {
   const int N = p.N;
-  const size_t total = (size_t)E_local * N;
+  constexpr int PT = VEC ? 4 : 1;
+  const size_t total = (size_t)E_local * N / PT;
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
-    const int e = (int)(o / N), k = (int)(o - (size_t)e * N);
+    const size_t o0 = o * PT;
+    const int e = (int)(o0 / N), k = (int)(o0 - (size_t)e * N);
     const size_t g = (size_t)(e + p.edge_offset) * N + k;
     const int ix = a.ii_rank[e], jx = a.jj_rank[e];
-    const bool vm = a.valid[g] != 0;
-    const int64_t ind = vm ? a.idx[g] : 0;
-    const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
-    const float q = a.Q[g];
-    const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
-                       (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
-    // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
-    const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
-    float4 r;
-    if constexpr (MODE == BA_MODE_CALIB) {
-      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
-      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
-      r = make_float4((float)u_t, (float)v_t, Xi[2], sw);
+    if constexpr (VEC) {
+      const uchar4 vm = *reinterpret_cast<const uchar4*>(a.valid + g);
+      const longlong2 i01 = *reinterpret_cast<const longlong2*>(a.idx + g);
+      const longlong2 i23 = *reinterpret_cast<const longlong2*>(a.idx + g + 2);
+      const float4 q = *reinterpret_cast<const float4*>(a.Q + g);
+      const float cs = a.Cscale[jx];
+      const float4 c = *reinterpret_cast<const float4*>(a.Ckf[jx] + k);
+      float4* r = a.rec + o0;
+      r[0] = ba_pack_point<MODE>(a, p, ix, jx, vm.x != 0, i01.x, q.x, c.x * cs);
+      r[1] = ba_pack_point<MODE>(a, p, ix, jx, vm.y != 0, i01.y, q.y, c.y * cs);
+      r[2] = ba_pack_point<MODE>(a, p, ix, jx, vm.z != 0, i23.x, q.z, c.z * cs);
+      r[3] = ba_pack_point<MODE>(a, p, ix, jx, vm.w != 0, i23.y, q.w, c.w * cs);
     } else {
-      r = make_float4(Xi[0], Xi[1], Xi[2], sw);
+      a.rec[o0] = ba_pack_point<MODE>(a, p, ix, jx, a.valid[g] != 0, a.idx[g], a.Q[g], a.Ckf[jx][k] * a.Cscale[jx]);
     }
-    a.rec[o] = r;
   }
 }
 
@@ -1055,14 +1074,25 @@ extern "C" int m3s_debug_sp_stamps(unsigned long long* out) {
 // ------------------------------------------------------------------------------------------
 extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
-  const size_t total = (size_t)E_local * p->N;
+  // the vector path needs 16-B aligned rows: N % 4 == 0 and aligned base pointers (idx 32-B rows of 4 points)
+  const bool vec = p->N % 4 == 0 && p->c_aligned && (reinterpret_cast<uintptr_t>(a->idx) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a->Q) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->valid) & 3) == 0;
+  const size_t total = (size_t)E_local * p->N / (vec ? 4 : 1);
   const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
+#define M3S_PACK(MODE)                                                                              \
+  do {                                                                                              \
+    if (vec)                                                                                        \
+      hipLaunchKernelGGL((m3s::ba_pack_kernel<MODE, true>), g, dim3(256), 0, s, *a, *p, E_local);  \
+    else                                                                                            \
+      hipLaunchKernelGGL((m3s::ba_pack_kernel<MODE, false>), g, dim3(256), 0, s, *a, *p, E_local); \
+  } while (0)
   if (p->mode == BA_MODE_CALIB)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, E_local);
+    M3S_PACK(BA_MODE_CALIB);
   else if (p->mode == BA_MODE_RAYS)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, E_local);
+    M3S_PACK(BA_MODE_RAYS);
   else
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, E_local);
+    M3S_PACK(BA_MODE_POINTS);
+#undef M3S_PACK
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ struct BaParams {
   float fx, fy, cx, cy;
   int H, W, pixel_border;
   float z_eps;
+  int c_aligned;  // every keyframe confidence row is 16-B aligned (the pack's 4-point vector path)
 };
 
 struct BaArgs {

@@ -19,3 +19,9 @@ print('value', d['value'], 'kernels', d['kernels_us'], 'frame', d['frame']['medi
 b=d['ba']; print('C5', {x: b[x] for x in ('edges_per_s','ms_per_call','ms_setup','ms_pack','ms_plan_host','ms_lin_per_iter','ms_solve_per_iter')}, b['roofline']['frac'])
 c=b['c4']; print('C4', {x: c[x] for x in ('edges_per_s','ms_per_call','ms_setup','ms_lin_per_iter','ms_solve_per_iter')}, c['roofline']['frac'])
 "; [ $rc -eq 0 ] || { tail -30 gpurun_out/bench.err; exit $rc; }
+for V in ${VARIANTS}; do
+  L=lightweight-mast3r-slam_amd/lib/exp/libm3s_$V.so; echo "== $V"
+  M3S_LIB=$L timeout -k 10 400 python3 -u scripts/ba_acc.py > gpurun_out/acc_$V.json 2> gpurun_out/acc_$V.err
+  echo "ACC_RC=$?"; cat gpurun_out/acc_$V.json
+  M3S_LIB=$L timeout -k 10 200 python3 scripts/ba_exp.py 256 320 512 10 euroc rays 2>&1 | grep "rep 1"
+done
