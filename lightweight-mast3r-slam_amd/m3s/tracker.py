@@ -17,6 +17,7 @@ import torch
 
 from m3s import _lib
 from m3s.config import config
+from m3s.frame import Frame
 from m3s.matching import match, match_halves
 from m3s.sim3 import Sim3
 
@@ -146,7 +147,10 @@ class FrameTracker:
         self.idx_f2k = idx_f2k
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
-        frame.update_pointmap(Xff, Cff, own=True)  # fresh model outputs: no clone (frame.py:41-45 clones)
+        if isinstance(frame, Frame):
+            frame.update_pointmap(Xff, Cff, own=True)  # fresh model outputs: no clone (frame.py:41-45 clones)
+        else:  # the reference's Frame (m3s/hook.py): its own update_pointmap
+            frame.update_pointmap(Xff, Cff)
 
         use_calib = config["use_calib"]
         img_size = frame_img_size(frame)
