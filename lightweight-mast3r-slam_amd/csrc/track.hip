@@ -309,8 +309,11 @@ typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gull;
 
-#define GN_THREADS 256
-#define GN_PPT 4     // points per thread per round: all their record loads issued before any math
+#ifndef GN_THREADS
+#define GN_THREADS 256  // threads of a GN block (one block per CU)
+#endif
+#define GN_PPT (1024 / GN_THREADS)  // points per thread per round (1024 per block): record loads issued before any math
+#define GN_MAX_BLOCKS 256           // partial rows per iteration slot
 
 // ---- the 36 fp64 sums of a wave, reduce-scattered over its lanes (deterministic, no LDS) ----
 // Six half-exchange steps: lanes l and l^32 (v_permlane32_swap: the two halves of a register pair trade places,
@@ -523,10 +526,12 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     __syncthreads();
     // the block partial: 36 threads add the 4 waves' totals, store it write-through into this iteration's slot
     const int slot = it % GN_SLOTS;
-    gdouble* part = (gdouble*)(a.partials + (size_t)slot * GN_THREADS * GN_PSTRIDE);
+    gdouble* part = (gdouble*)(a.partials + (size_t)slot * GN_MAX_BLOCKS * GN_PSTRIDE);
     if (threadIdx.x < GN_NSUM) {
       const int l = gn_lane_of(threadIdx.x);
-      const double v = ((s_w[0][l] + s_w[1][l]) + s_w[2][l]) + s_w[3][l];
+      double v = s_w[0][l];
+#pragma unroll
+      for (int w = 1; w < GN_THREADS / 64; w++) v += s_w[w][l];
       __hip_atomic_store(&part[(size_t)blockIdx.x * GN_PSTRIDE + threadIdx.x], v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
