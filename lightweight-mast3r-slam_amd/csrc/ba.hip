@@ -72,18 +72,22 @@ __device__ __forceinline__ f2 huber_ba2(f2 r) {
   return ra < KH ? f2{1.0f, 1.0f} : q;
 }
 
-// 1/sqrt(x) and 1/x of two values: the hardware estimates (~1 ulp), with BA_RAYS_NEWTON one Newton step each
-// (packed), which takes out the estimates' bias against the reference's IEEE sqrtf and divisions
+// 1/sqrt(x) and 1/x of two values: the hardware estimates (~1 ulp) refined by one Newton step each (packed), which
+// takes out the estimates' bias against the reference's IEEE sqrtf and divisions: without it the K = 256 EuRoC rays
+// graph sat 1.14e-5 from the fp64 truth (6.8e-6 with it, for +2 % linearisation time; scripts/ba_acc.py)
+#ifndef BA_RAYS_NEWTON
+#define BA_RAYS_NEWTON 1
+#endif
 __device__ __forceinline__ f2 rsq2(f2 x) {
   f2 y = {__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)};
-#ifdef BA_RAYS_NEWTON
+#if BA_RAYS_NEWTON
   y = y * __builtin_elementwise_fma(-0.5f * x * y, y, f2{1.5f, 1.5f});
 #endif
   return y;
 }
 __device__ __forceinline__ f2 rcp2(f2 x) {
   f2 y = {__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
-#ifdef BA_RAYS_NEWTON
+#if BA_RAYS_NEWTON
   y = y * __builtin_elementwise_fma(-x, y, f2{2.0f, 2.0f});
 #endif
   return y;
@@ -1075,8 +1079,14 @@ extern "C" int m3s_debug_sp_stamps(unsigned long long* out) {
 extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
   // the vector path needs 16-B aligned rows: N % 4 == 0 and aligned base pointers (idx 32-B rows of 4 points)
+  // the 4-point vector path measured 2.25x SLOWER on MI355X (C5 pack 4.1 -> 9.3 ms: four dependent gather chains
+  // per thread and a quarter of the threads in flight); kept selectable for experiments (M3S_BA_PACK_VEC builds)
+#ifdef M3S_BA_PACK_VEC
   const bool vec = p->N % 4 == 0 && p->c_aligned && (reinterpret_cast<uintptr_t>(a->idx) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(a->Q) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->valid) & 3) == 0;
+#else
+  const bool vec = false;
+#endif
   const size_t total = (size_t)E_local * p->N / (vec ? 4 : 1);
   const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
 #define M3S_PACK(MODE)                                                                              \

@@ -17,3 +17,12 @@ import json; d=json.loads(open('gpurun_out/bench_$V.json').read().strip().splitl
 print('value', round(d['value']), 'kernels', d['kernels_us'], 'frame median', round(d['frame']['median_ms'], 4), 'iters', d['config']['gn_iters_mean'])
 "; [ $rc -eq 0 ] || exit $rc
 done
+# BA solve A/B: this tree's factorisation vs round 2's (libm3s_r2: round-2 ba.hip, 16-wave cost model)
+for V in main r2; do
+  if [ "$V" = main ]; then L=lightweight-mast3r-slam_amd/lib/libm3s.so; S=lightweight-mast3r-slam_amd/lib/exp/libm3s_spst.so;
+  else L=lightweight-mast3r-slam_amd/lib/exp/libm3s_$V.so; S=lightweight-mast3r-slam_amd/lib/exp/libm3s_${V}st.so; fi
+  echo "== solve $V"
+  M3S_LIB=$L timeout -k 10 200 python3 scripts/ba_exp.py 256 384 512 10 chess calib 2>&1 | grep "rep 1" || exit 1
+  M3S_LIB=$L timeout -k 10 200 python3 scripts/ba_exp.py 256 320 512 10 euroc rays 2>&1 | grep "rep 1" || exit 1
+  M3S_LIB=$S timeout -k 10 200 python3 scripts/ba_exp.py 256 384 512 3 chess calib 2>&1 | grep -E "factor stamps|root-end"
+done
