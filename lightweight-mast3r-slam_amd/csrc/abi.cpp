@@ -908,8 +908,6 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.p.W = cfg->width;
   P.p.pixel_border = cfg->pixel_border;
   P.p.z_eps = cfg->z_eps;
-  P.p.c_aligned = 1;
-  for (int k = 0; k < Kp; k++) P.p.c_aligned &= (reinterpret_cast<uintptr_t>(Ch[k]) & 15) == 0;
   P.Kp = Kp;
   P.N = N;
   P.E = E;

@@ -144,73 +144,36 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
   }
 }
 
-#ifdef BA_V_RUN  // (experiment) a shorter fp32 run for the 7 gradient sums only: the odd lane owns them (18..34)
-__device__ __forceinline__ void pair_flush_v(double* acc, f2* fv, bool odd) {
-#pragma unroll
-  for (int c = 28; c < 35; c++) {
-    const int m = c - BA_PAIR_HALF;
-    const f2 own = fv[c - 28];
-    const f2 got = {dpp_swap1(own.x), dpp_swap1(own.y)};
-    if (odd) {
-      acc[m] += (double)own.x;
-      acc[m] += (double)own.y;
-      acc[m] += (double)got.x;
-      acc[m] += (double)got.y;
-    }
-    fv[c - 28] = f2{0.0f, 0.0f};
-  }
-}
-#endif
-
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
 //   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
 //   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
 //   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
 template <int MODE>
-__device__ __forceinline__ float4 ba_pack_point(const BaArgs& a, const BaParams& p, int ix, int jx, bool vm,
-                                               int64_t ind, float q, float cj) {
-  ind = vm ? ind : 0;
-  const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
-  const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) && (cj > p.C_thresh);
-  // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
-  const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
-  if constexpr (MODE == BA_MODE_CALIB) {
-    const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
-    const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
-    return make_float4((float)u_t, (float)v_t, Xi[2], sw);
-  } else {
-    return make_float4(Xi[0], Xi[1], Xi[2], sw);
-  }
-}
-
-// VEC: 4 consecutive points per thread (N % 4 == 0): the per-point streams (valid, idx, Q, C_j) are read as 4-, 32-,
-// 16- and 16-byte vectors and the records written as four 16-byte stores, instead of one small access per point
-template <int MODE, bool VEC>
 __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int E_local) {
   const int N = p.N;
-  constexpr int PT = VEC ? 4 : 1;
-  const size_t total = (size_t)E_local * N / PT;
+  const size_t total = (size_t)E_local * N;
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
-    const size_t o0 = o * PT;
-    const int e = (int)(o0 / N), k = (int)(o0 - (size_t)e * N);
+    const int e = (int)(o / N), k = (int)(o - (size_t)e * N);
     const size_t g = (size_t)(e + p.edge_offset) * N + k;
     const int ix = a.ii_rank[e], jx = a.jj_rank[e];
-    if constexpr (VEC) {
-      const uchar4 vm = *reinterpret_cast<const uchar4*>(a.valid + g);
-      const longlong2 i01 = *reinterpret_cast<const longlong2*>(a.idx + g);
-      const longlong2 i23 = *reinterpret_cast<const longlong2*>(a.idx + g + 2);
-      const float4 q = *reinterpret_cast<const float4*>(a.Q + g);
-      const float cs = a.Cscale[jx];
-      const float4 c = *reinterpret_cast<const float4*>(a.Ckf[jx] + k);
-      float4* r = a.rec + o0;
-      r[0] = ba_pack_point<MODE>(a, p, ix, jx, vm.x != 0, i01.x, q.x, c.x * cs);
-      r[1] = ba_pack_point<MODE>(a, p, ix, jx, vm.y != 0, i01.y, q.y, c.y * cs);
-      r[2] = ba_pack_point<MODE>(a, p, ix, jx, vm.z != 0, i23.x, q.z, c.z * cs);
-      r[3] = ba_pack_point<MODE>(a, p, ix, jx, vm.w != 0, i23.y, q.w, c.w * cs);
+    const bool vm = a.valid[g] != 0;
+    const int64_t ind = vm ? a.idx[g] : 0;
+    const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
+    const float q = a.Q[g];
+    const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
+                       (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
+    // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
+    const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
+    float4 r;
+    if constexpr (MODE == BA_MODE_CALIB) {
+      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
+      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
+      r = make_float4((float)u_t, (float)v_t, Xi[2], sw);
     } else {
-      a.rec[o0] = ba_pack_point<MODE>(a, p, ix, jx, a.valid[g] != 0, a.idx[g], a.Q[g], a.Ckf[jx][k] * a.Cscale[jx]);
+      r = make_float4(Xi[0], Xi[1], Xi[2], sw);
     }
+    a.rec[o] = r;
   }
 }
 
@@ -341,9 +304,6 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
     }
-#if defined(BA_V_RUN) && BA_PAIR_ACC
-    if ((run + 1) % BA_V_RUN == 0 && run + 1 != BA_RUN_LEN) pair_flush_v(acc, fv, odd);
-#endif
     if (++run == BA_RUN_LEN) {  // the run's fp32 sums (BA_RUN_LEN points per slot) into the fp64 accumulators
       run = 0;
 #if BA_PAIR_ACC
@@ -537,8 +497,7 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL) {
   *out = s;
 }
 
-constexpr int SP_WAVES = M3S_BA_SP_WAVES;    // waves of the factor workgroup (256-VGPR budget at 8 waves)
-constexpr int SP_THREADS = SP_WAVES * 64;
+constexpr int SP_WAVES = 16;                 // waves of the factor workgroup
 constexpr int SP_PLAN_BYTES = 144 * 1024;   // LDS for the plan's loop tables and the solution x
 
 // 1/sqrt(d) for d > 0: the v_rsq_f64 estimate (~2^-22 relative) refined by ONE Newton step (~2^-44)
@@ -581,14 +540,9 @@ __device__ unsigned long long g_sp_stamps[4096];
   do {                                                                                        \
     if (threadIdx.x == 0 && (k) < 3000) g_sp_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-// FST(k): phase k of ONE task (column a.nb - 2's factor task, FSTJ = that column), every load of the
-// wave drained first so the stamp falls after the data arrived
 #define FST(k)                                                                              \
   do {                                                                                      \
-    if (fst_on) {                                                                           \
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                          \
-      if (lane == 0) g_sp_stamps[3000 + (k)] = __builtin_amdgcn_s_memrealtime();          \
-    }                                                                                       \
+    if (lane == 0) g_sp_stamps[3000 + (k)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
 #else
 #define SPST(k) \
@@ -758,100 +712,44 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int noff = b1 - b0 - 1, nrow = 7 * (noff + 1) + 1;
   const bool has1 = lane < nrow, has2 = lane + 64 < nrow;
-#ifdef M3S_SP_STAMPS
-  const bool fst_on = j == a.nb - 2;
-#endif
-  FST(0);
   double v1[8], v2[8];
   double* p1 = has1 ? sp_row_addr(a, b0, noff, j, lane) : nullptr;
   double* p2 = has2 ? sp_row_addr(a, b0, noff, j, lane + 64) : nullptr;
   if (has1) ld_row(v1, p1);
   if (has2) ld_row(v2, p2);
-  FST(1);
   const int g = T.pull_grp[j];
   if (g >= 0) sp_group_regs(a, T, g, noff, nrow, v1, v2, lane, bjk);
-  FST(2);
-  // the 7x7 diagonal block: its rows (lanes 0..6) go through LDS and EVERY lane factors it redundantly in
-  // registers (left-looking; no cross-lane broadcasts on the pivot chain), then each lane solves its own rows
-  // x L_jj^T = a (the off-diagonal rows give L_ij, the rhs row the forward substitution y_j = L_jj^-1 b_j)
-  if (lane < 7) {
-#pragma unroll
-    for (int c = 0; c < 7; c++)
-      if (c <= lane) bjk[lane * 7 + c] = v1[c];
-  }
-  wave_sync();
   bool fail = false;
-  double inv[7], lo[21], ldg[7];  // lo[r (r - 1) / 2 + c] = L[r][c] (c < r), ldg[m] = L[m][m]
+  double inv[7], lo[21];
 #pragma unroll
   for (int m = 0; m < 7; m++) {
-    double d = bjk[m * 7 + m];
-#pragma unroll
-    for (int k = 0; k < m; k++) d = fma(-lo[m * (m - 1) / 2 + k], lo[m * (m - 1) / 2 + k], d);
+    double d = bcast_lane(v1[m], m);
     if (!(d > 0.0)) {  // not positive definite: the step is discarded (dx = 0), as SimplicialLLT's info
       fail = true;
       d = 1.0;
     }
     inv[m] = rsqrt_nr(d);
-    ldg[m] = d * inv[m];
+    const double l1 = v1[m] * inv[m], l2 = v2[m] * inv[m];
+    v1[m] = lane == m ? d * inv[m] : l1;
+    v2[m] = l2;
 #pragma unroll
-    for (int r = m + 1; r < 7; r++) {
-      double t = bjk[r * 7 + m];
-#pragma unroll
-      for (int k = 0; k < m; k++) t = fma(-lo[r * (r - 1) / 2 + k], lo[m * (m - 1) / 2 + k], t);
-      lo[r * (r - 1) / 2 + m] = t * inv[m];
+    for (int c = m + 1; c < 7; c++) {
+      const double lc = bcast_lane(l1, c);
+      lo[c * (c - 1) / 2 + m] = lc;
+      v1[c] = fma(-l1, lc, v1[c]);
+      v2[c] = fma(-l2, lc, v2[c]);
     }
-  }
-  wave_sync();  // bjk is free again
-  // own rows: the diagonal rows take L (lower), every other row solves x L^T = a (in order m = 0..6)
-#pragma unroll
-  for (int m = 0; m < 7; m++) {
-    double t1 = v1[m], t2 = v2[m];
-#pragma unroll
-    for (int k = 0; k < m; k++) {
-      t1 = fma(-v1[k], lo[m * (m - 1) / 2 + k], t1);
-      t2 = fma(-v2[k], lo[m * (m - 1) / 2 + k], t2);
-    }
-    v1[m] = t1 * inv[m];
-    v2[m] = t2 * inv[m];
-  }
-#pragma unroll
-  for (int r = 0; r < 7; r++) {
-#pragma unroll
-    for (int c = 0; c < r; c++) v1[c] = lane == r ? lo[r * (r - 1) / 2 + c] : v1[c];
-    v1[r] = lane == r ? ldg[r] : v1[r];
   }
   if (fail && lane == 0) *bad = 1;
-  if (lane < 7) {
-    // L_jj^-1 for the back substitution, off its chain: lane c forward-substitutes e_c (column c of the inverse,
-    // zero above row c) and keeps (L_jj^-1)[i][c], i > c, in the strictly upper part of its own row of the
-    // diagonal block (block[c][i], unused by the factorisation) and 1/L_cc = (L_jj^-1)[c][c] in column 7
-    double col[7];
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-      double acc = lane == i ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < i; k++) acc = fma(-lo[i * (i - 1) / 2 + k], col[k], acc);
-      col[i] = acc * inv[i];
-    }
-#pragma unroll
-    for (int i = 1; i < 7; i++)
-      if (i > lane) v1[i] = col[i];
+  if (lane < 7) {  // 1/L_mm in column 7 of the diagonal block (used by the back substitution)
     double iv = inv[0];
 #pragma unroll
     for (int m = 1; m < 7; m++) iv = lane == m ? inv[m] : iv;
     v1[7] = iv;
   }
-  FST(3);
   if (has1) st_row(p1, v1);
   if (has2) st_row(p2, v2);
   if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, g, lo, inv, lane, bjk);
-  FST(4);
-#ifdef M3S_SP_STAMPS
-  if (fst_on && lane == 0) {
-    g_sp_stamps[3010] = noff;
-    g_sp_stamps[3011] = g >= 0 ? T.grp[g].z - T.grp[g].y : 0;
-  }
-#endif
 }
 
 // B. update group g (one wave): the rows of its target column take the group's sources, loaded and
@@ -873,44 +771,24 @@ __device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables&
 }
 
 // back substitution of column j: x_j = L_jj^-T (y_j - sum_{i in struct(j)} L_ij^T x_i); X = the solution
-// (LDS when it fits), 8 doubles per column. Everything it reads from the factor is final before the back
-// substitution starts, so a wave loads its NEXT column's data (SpBack) while it solves the current one: only
-// the x_i of the ancestors (LDS) sit on the level-to-level chain.
-struct SpBack {
-  double dr[8];  // lane m < 7: row m of the diagonal block = (L_jj^-1)[i][m] (i > m) | 1/L_mm (column 7)
-  double lb[7];  // lane (q, m), q = lane / 7: column m of off-diagonal block b0 + 1 + q (rows 0..6)
-  double yv;     // lane < 7: the forward-substituted rhs y_j
-  int xrow;      // that block's row (index into X), -1 when the lane has no block
-};
-
-__device__ __forceinline__ SpBack sp_back_load(const BaArgs& a, const SpTables& T, int j, int lane) {
-  SpBack d;
+// (LDS when it fits), 8 doubles per column
+__device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& T, double* X, int j, int lane,
+                                               double* red) {
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int q = lane / 7, m = lane - 7 * (lane / 7);
+  const double* D = a.L + (size_t)b0 * 64;
+  double dl[8][8];  // L_jj (lower) and 1/L_mm (column 7), issued before the sums
 #pragma unroll
-  for (int c = 0; c < 8; c++) d.dr[c] = 0.0;
-  if (lane < 7) ld_row(d.dr, a.L + (size_t)b0 * 64 + lane * 8);
-  d.yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
-  const int b = b0 + 1 + q;
-  d.xrow = (lane < 63 && b < b1) ? T.rowL[b] : -1;
-  const double* Lb = a.L + (size_t)(d.xrow >= 0 ? b : b0) * 64 + m;
+  for (int r = 0; r < 7; r++) {
+    double row[8];
+    ld_row(row, D + r * 8);
 #pragma unroll
-  for (int r = 0; r < 7; r++) d.lb[r] = d.xrow >= 0 ? Lb[r * 8] : 0.0;
-  return d;
-}
-
-__device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& T, double* X, int j, const SpBack& d,
-                                               int lane, double* red) {
-  const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
-  const int q = lane / 7, m = lane - 7 * (lane / 7);
-  double acc = 0.0;
-  if (d.xrow >= 0) {
-    const double* xi = X + (size_t)d.xrow * 8;
-#pragma unroll
-    for (int r = 0; r < 7; r++) acc = fma(d.lb[r], xi[r], acc);
+    for (int c = 0; c < 8; c++) dl[r][c] = row[c];
   }
-  if (lane < 63)  // columns of more than 9 off-diagonal blocks: the rest, loaded here
-    for (int b = b0 + 1 + q + 9; b < b1; b += 9) {
+  const double yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
+  double acc = 0.0;
+  if (lane < 63)
+    for (int b = b0 + 1 + q; b < b1; b += 9) {
       const double* Lb = a.L + (size_t)b * 64 + m;
       const double* xi = X + (size_t)T.rowL[b] * 8;
 #pragma unroll
@@ -919,18 +797,26 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
   red[lane] = acc;
   wave_sync();
   if (lane < 7) {
-    double sacc = d.yv;
+    double sacc = yv;
 #pragma unroll
     for (int qq = 0; qq < 9; qq++) sacc -= red[qq * 7 + lane];  // fixed order: deterministic
     red[lane] = sacc;
   }
   wave_sync();
-  if (lane < 7) {  // x_m = sum_{i >= m} (L_jj^-1)[i][m] z_i: seven independent dot products
-    double x = d.dr[7] * red[lane];
+  double z[7];
 #pragma unroll
-    for (int i = 1; i < 7; i++)
-      if (i > lane) x = fma(d.dr[i], red[i], x);
-    X[(size_t)j * 8 + lane] = x;
+  for (int mm = 0; mm < 7; mm++) z[mm] = red[mm];
+  double x[7];
+#pragma unroll
+  for (int mm = 6; mm >= 0; mm--) {
+    double vv = z[mm];
+#pragma unroll
+    for (int p = mm + 1; p < 7; p++) vv = fma(-dl[p][mm], x[p], vv);
+    x[mm] = vv * dl[mm][7];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) X[(size_t)j * 8 + mm] = x[mm];
   }
   wave_sync();
 }
@@ -953,7 +839,7 @@ __global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int l) {
 }
 
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
-__global__ void __launch_bounds__(SP_THREADS) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
+__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
   __shared__ __attribute__((aligned(16))) int s_plan[LT ? SP_PLAN_BYTES / 4 : 4];
   __shared__ double s_red[SP_WAVES][64];  // per-wave staging: L_jk and the back-substitution sums
@@ -968,12 +854,12 @@ __global__ void __launch_bounds__(SP_THREADS) ba_sparse_factor_kernel(BaArgs a, 
     int4* dst = reinterpret_cast<int4*>(s_plan);
     const int n16 = (a.plan_bytes + 15) / 16;
     int4 tmp[8];
-    for (int i0 = 0; i0 < n16; i0 += 8 * SP_THREADS) {
+    for (int i0 = 0; i0 < n16; i0 += 8 * 1024) {
 #pragma unroll
-      for (int u = 0; u < 8; u++) tmp[u] = src[min(i0 + u * SP_THREADS + (int)threadIdx.x, n16 - 1)];
+      for (int u = 0; u < 8; u++) tmp[u] = src[min(i0 + u * 1024 + (int)threadIdx.x, n16 - 1)];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * SP_THREADS + (int)threadIdx.x;
+        const int i = i0 + u * 1024 + (int)threadIdx.x;
         if (i < n16) dst[i] = tmp[u];
       }
     }
@@ -998,40 +884,14 @@ __global__ void __launch_bounds__(SP_THREADS) ba_sparse_factor_kernel(BaArgs a, 
     SPST(2 + l);
   }
   // back substitution, levels from the root down; runs of single-column levels stay on wave 0 with no
-  // barrier between them (X in LDS: a wave's LDS accesses are ordered). Each wave walks its columns (c0 + w,
-  // c0 + w + 16, ... of every level) in order and loads the next one's factor data ahead (SpBack).
-  {
-    // the wave's next task at or below level l starting from index c (-1: none)
-    auto next_task = [&](int l, int c, int* nl) -> int {
-      for (; l >= 0; l--) {
-        const int lo_c = T.lev_ptr[l], hi_c = T.lev_ptr[l + 1];
-        if (c < 0) c = lo_c + w;
-        if (c < hi_c) {
-          *nl = l;
-          return c;
-        }
-        c = -1;
-      }
-      return -1;
-    };
-    int pl = 0;
-    int pc = next_task(nlev - 1, -1, &pl);
-    SpBack pre = sp_back_load(a, T, pc >= 0 ? T.lev_col[pc] : 0, lane);
-    for (int l = nlev - 1; l >= 0; l--) {
-      const int c0 = T.lev_ptr[l], c1 = T.lev_ptr[l + 1];
-      for (int c = c0 + w; c < c1; c += SP_WAVES) {  // == (pl, pc)
-        const SpBack cur = pre;
-        const int j = T.lev_col[c];
-        int nl = 0;
-        pc = next_task(l, c + SP_WAVES, &nl);
-        if (pc >= 0) pre = sp_back_load(a, T, T.lev_col[pc], lane);  // in flight during this column
-        sp_back_column(a, T, X, j, cur, lane, s_red[w]);
-      }
-      const bool chain = LT && c1 - c0 == 1 && l > 0 && T.lev_ptr[l] - T.lev_ptr[l - 1] == 1;
-      if (!chain) {
-        __syncthreads();
-        SPST(3 + nlev + (nlev - 1 - l));
-      }
+  // barrier between them (X in LDS: a wave's LDS accesses are ordered)
+  for (int l = nlev - 1; l >= 0; l--) {
+    const int c0 = T.lev_ptr[l], c1 = T.lev_ptr[l + 1];
+    for (int c = c0 + w; c < c1; c += SP_WAVES) sp_back_column(a, T, X, T.lev_col[c], lane, s_red[w]);
+    const bool chain = LT && c1 - c0 == 1 && l > 0 && T.lev_ptr[l] - T.lev_ptr[l - 1] == 1;
+    if (!chain) {
+      __syncthreads();
+      SPST(3 + nlev + (nlev - 1 - l));
     }
   }
   __syncthreads();
@@ -1039,14 +899,14 @@ __global__ void __launch_bounds__(SP_THREADS) ba_sparse_factor_kernel(BaArgs a, 
   const bool failed = s_bad != 0 || (a.wide_steps > 0 && *a.bad != 0);
   const int n = a.nb * 7;
   float n2 = 0.0f;
-  for (int i = threadIdx.x; i < n; i += SP_THREADS) {
+  for (int i = threadIdx.x; i < n; i += 1024) {
     const int j = i / 7, m = i - 7 * (i / 7);
     const float d = failed ? 0.0f : (float)(-X[(size_t)j * 8 + m]);
     a.dx[a.perm[j] * 7 + m] = d;
     n2 += d * d;
   }
   __syncthreads();
-  for (int k = 1 + threadIdx.x; k < K; k += SP_THREADS) {
+  for (int k = 1 + threadIdx.x; k < K; k += 1024) {
     float Tw[8], xi[7];
     for (int c = 0; c < 8; c++) Tw[c] = a.Twc[k * 8 + c];
     for (int c = 0; c < 7; c++) xi[c] = a.dx[(k - 1) * 7 + c];
@@ -1078,31 +938,14 @@ extern "C" int m3s_debug_sp_stamps(unsigned long long* out) {
 // ------------------------------------------------------------------------------------------
 extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
-  // the vector path needs 16-B aligned rows: N % 4 == 0 and aligned base pointers (idx 32-B rows of 4 points)
-  // the 4-point vector path measured 2.25x SLOWER on MI355X (C5 pack 4.1 -> 9.3 ms: four dependent gather chains
-  // per thread and a quarter of the threads in flight); kept selectable for experiments (M3S_BA_PACK_VEC builds)
-#ifdef M3S_BA_PACK_VEC
-  const bool vec = p->N % 4 == 0 && p->c_aligned && (reinterpret_cast<uintptr_t>(a->idx) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(a->Q) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->valid) & 3) == 0;
-#else
-  const bool vec = false;
-#endif
-  const size_t total = (size_t)E_local * p->N / (vec ? 4 : 1);
+  const size_t total = (size_t)E_local * p->N;
   const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
-#define M3S_PACK(MODE)                                                                              \
-  do {                                                                                              \
-    if (vec)                                                                                        \
-      hipLaunchKernelGGL((m3s::ba_pack_kernel<MODE, true>), g, dim3(256), 0, s, *a, *p, E_local);  \
-    else                                                                                            \
-      hipLaunchKernelGGL((m3s::ba_pack_kernel<MODE, false>), g, dim3(256), 0, s, *a, *p, E_local); \
-  } while (0)
   if (p->mode == BA_MODE_CALIB)
-    M3S_PACK(BA_MODE_CALIB);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, E_local);
   else if (p->mode == BA_MODE_RAYS)
-    M3S_PACK(BA_MODE_RAYS);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, E_local);
   else
-    M3S_PACK(BA_MODE_POINTS);
-#undef M3S_PACK
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, E_local);
   return hipGetLastError();
 }
 
@@ -1126,8 +969,8 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
   for (int l = 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0) hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, l);
   if (((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 <= (size_t)m3s::SP_PLAN_BYTES)
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(m3s::SP_THREADS), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(m3s::SP_THREADS), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   return hipGetLastError();
 }

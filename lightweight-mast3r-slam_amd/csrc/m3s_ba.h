@@ -8,7 +8,7 @@
 #define BA_MODE_CALIB 2
 
 #ifndef M3S_BA_SP_WAVES
-#define M3S_BA_SP_WAVES 8  // waves of the one-workgroup sparse factorisation (ba.hip) and of its cost model (abi.cpp)
+#define M3S_BA_SP_WAVES 16  // waves of the one-workgroup sparse factorisation (ba.hip) and of its cost model (abi.cpp)
 #endif
 
 struct BaParams {
@@ -21,7 +21,6 @@ struct BaParams {
   float fx, fy, cx, cy;
   int H, W, pixel_border;
   float z_eps;
-  int c_aligned;  // every keyframe confidence row is 16-B aligned (the pack's 4-point vector path)
 };
 
 struct BaArgs {

@@ -40,6 +40,9 @@ typedef __attribute__((address_space(3))) void* lvoid_t;
 #ifdef M3S_REFINE_STATS  // (experiment builds only) per-level deferred lanes / waves
 __device__ unsigned long long g_refine_stats[32];
 #endif
+#ifdef M3S_REFINE_BSTAMPS  // (experiment builds only) per-block start / end s_memrealtime, hardware id, active lanes
+__device__ unsigned long long g_refine_bstamps[8192 * 4];
+#endif
 
 // One level of one pixel by the whole wave (cu, cv, max_score, sq wave-uniform): lane c < 49 scores
 // candidate (c / 7, c % 7) from global memory; the first candidate in scan order holding the wave
@@ -307,6 +310,9 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
     t.fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
   }
   const bool mine = active;  // deferred pixels are written by refine_outlier_kernel
+#ifdef M3S_REFINE_BSTAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_refine_bstamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
   h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
   for (int d = dilation_max; d > 0; d--) {
     switch (d) {
@@ -321,6 +327,19 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
     }
   }
   if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
+#ifdef M3S_REFINE_BSTAMPS
+  const unsigned long long nact = __popcll(__ballot(active));
+  __shared__ unsigned long long s_act[4];
+  if (t.lane == 0) s_act[t.wid] = nact;
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_refine_bstamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    g_refine_bstamps[blockIdx.x * 4 + 2] = hw;
+    g_refine_bstamps[blockIdx.x * 4 + 3] = s_act[0] + s_act[1] + s_act[2] + s_act[3];
+  }
+#endif
 }
 
 // Finishes the deferred pixels: one wave per pixel, levels d0..1 by wave_level (grid-stride over
@@ -394,6 +413,13 @@ extern "C" hipError_t m3s_launch_refine_tile(const void* D11h, const void* D21, 
   return hipGetLastError();
 }
 
+#ifdef M3S_REFINE_BSTAMPS
+extern "C" int m3s_debug_refine_bstamps(unsigned long long* out) {
+  (void)hipDeviceSynchronize();
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_refine_bstamps), sizeof(unsigned long long) * 8192 * 4) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 #ifdef M3S_REFINE_STATS
 extern "C" int m3s_debug_refine_stats(unsigned long long* out, int reset) {
   (void)hipDeviceSynchronize();

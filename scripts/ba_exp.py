@@ -78,6 +78,3 @@ if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the la
           f"back {t[3 + 2 * nlev] - t[2 + nlev]:.1f} us, tail {t[4 + 2 * nlev] - t[3 + 2 * nlev]:.1f} us, "
           f"total {t[4 + 2 * nlev]:.1f}")
     print("steps:", " ".join(f"{x:.2f}" for x in steps))
-    f = [(buf[3000 + k] - buf[3000]) / 100.0 for k in range(5)]
-    print(f"root-end factor task (column nb-2: {buf[3010]} off-diagonal blocks, {buf[3011]} pull sources), us from its "
-          f"start: rows loaded {f[1]:.2f}, pull group {f[2]:.2f}, factorised {f[3]:.2f}, stored {f[4]:.2f}")

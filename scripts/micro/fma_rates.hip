@@ -55,6 +55,12 @@ KERNEL(k_mul_f16, unsigned, "v_mul_f16 %0, %0, %1")
 KERNEL(k_cvt_f16_f32, unsigned, "v_cvt_f16_f32 %0, %1")
 KERNEL(k_cvt_f32_f16, unsigned, "v_cvt_f32_f16 %0, %1")
 KERNEL(k_perm_b32, unsigned, "v_perm_b32 %0, %0, %1, %1")
+// encodings of the same f16 add: VOP3 (e64) and SDWA (high-half source, high-half destination with the low half kept)
+KERNEL(k_add_f16_e64, unsigned, "v_add_f16_e64 %0, %0, %1")
+KERNEL(k_add_f16_sdwa_s1, unsigned, "v_add_f16_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1")
+KERNEL(k_add_f16_sdwa_d1, unsigned, "v_add_f16_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1")
+KERNEL(k_pack_b32_f16, unsigned, "v_pack_b32_f16 %0, %0, %1")
+KERNEL(k_add_f32_e64, float, "v_add_f32_e64 %0, %0, %1")
 // 64-bit operands
 KERNEL(k_pk_fma_f32, double, "v_pk_fma_f32 %0, %0, %1, %1")
 KERNEL(k_pk_mul_f32, double, "v_pk_mul_f32 %0, %0, %1")
@@ -83,15 +89,18 @@ int main() {
       {"v_pk_fma_f16", (const void*)k_pk_fma_f16, 4}, {"v_add_f16", (const void*)k_add_f16, 4},
       {"v_mul_f16", (const void*)k_mul_f16, 4},       {"v_cvt_f16_f32", (const void*)k_cvt_f16_f32, 4},
       {"v_cvt_f32_f16", (const void*)k_cvt_f32_f16, 4}, {"v_perm_b32", (const void*)k_perm_b32, 4},
+      {"v_add_f16_e64", (const void*)k_add_f16_e64, 4}, {"v_add_f16_sdwa_s1", (const void*)k_add_f16_sdwa_s1, 4},
+      {"v_add_f16_sdwa_d1", (const void*)k_add_f16_sdwa_d1, 4}, {"v_pack_b32_f16", (const void*)k_pack_b32_f16, 4},
+      {"v_add_f32_e64", (const void*)k_add_f32_e64, 4},
       {"v_fma_f64", (const void*)k_fma_f64, 8},       {"v_add_f64", (const void*)k_add_f64, 8},
   };
   const int iters = 4000;
   printf("gfx950 VALU issue cost per wave64 instruction per SIMD (median over %d CUs, one block per CU):\n"
          "s_memtime cycles | ns (s_memrealtime, 100 MHz) | cycles at 2.4 GHz from the ns\n", blocks);
-  printf("%-15s %26s %26s %26s\n", "instruction", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
+  printf("%-18s %26s %26s %26s\n", "instruction", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
   std::vector<unsigned long long> h(2 * blocks), hc(blocks), hr(blocks);
   for (const K& k : ks) {
-    printf("%-15s", k.name);
+    printf("%-18s", k.name);
     for (int T : {256, 512, 1024}) {
       void* args[] = {&out, &cyc, (void*)&iters};
       (void)args;
