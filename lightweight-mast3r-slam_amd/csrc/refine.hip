@@ -24,7 +24,11 @@
 //     op path, no workspace) the wave scores its outliers in place, one at a time (wave_level).
 //   * Tiles are dealt to XCDs in contiguous runs (bijective remap) so each XCD's 4 MiB L2 holds
 //     its slab of D11.
-// Compiled with -ffp-contract=off.
+// Compiled with -ffp-contract=off and -fno-slp-vectorize: each candidate's half sum stays a scalar chain (VOP2
+// v_add_f16 for the even channel, SDWA v_add_f16 for the odd one) instead of the SLP vectoriser pairing two
+// candidates per v_pk_add_f16 behind v_perm / v_pack transposes. Measured issue costs on gfx950 at 4 waves/SIMD
+// (scripts/micro/fma_rates, profiles/r03_valu_issue_rates.txt): VOP2 f16 add 1.18 ns, SDWA / VOP3P / v_perm
+// 2.03-2.09 ns per wave-instruction, so 2.67 ns per channel-candidate against 3.1 ns paired: 125 -> 116 us.
 #include "m3s_half.hpp"
 
 namespace m3s {
