@@ -7,4 +7,4 @@ mkdir -p gpurun_out
 bash scripts/gpu_check.sh || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err
 rc=$?; echo "BENCH_RC=$rc"; tail -c 400 gpurun_out/bench_default.json; [ $rc -eq 0 ] || exit $rc
-TAG=${TAG:-r02} bash scripts/gpu_prof_round.sh
+TAG=${TAG:-r03} bash scripts/gpu_prof_round.sh
