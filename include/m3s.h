@@ -109,6 +109,35 @@ int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyfr
                         const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
                         const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out, void* workspace,
                         size_t workspace_bytes, m3s_ba_plan* plan, void* stream);
+/* Record reuse across successive plans on ONE workspace (no reference counterpart; the reference backend calls
+ * solve_GN once per new keyframe, main.py:150-155, and re-gathers every edge each time). Between two such calls
+ * the edge set only grows and tracking changes only the keyframes it fuses into, so most edges' point records
+ * (ba_pack: matched point or pixel + folded validity weight) are still valid in the workspace. With reuse ids a
+ * plan packs only the edges that are new to the workspace or touch a keyframe whose points, confidences or
+ * fusion count changed since the workspace's previous plan (an exact bit compare on the device against copies
+ * the library keeps per keyframe); the other edges keep their records. Results are bit-identical to the plain
+ * plan. edge_uid (E entries, host): a stable id per directed edge naming immutable match data (its idx / valid /
+ * Q rows; FactorGraph uses 2u + direction for undirected edge u); kf_uid (Kp entries, host): a stable id per
+ * pose rank (the keyframe's global index). Contract: between reuse plans the workspace holds nothing else (a
+ * plain plan on it drops the cache); call m3s_ba_reuse_release(workspace) before freeing or repurposing it
+ * (frees the keyframe copies, 16 B per keyframe point). */
+typedef struct m3s_ba_reuse {
+  const int64_t* edge_uid;
+  const int64_t* kf_uid;
+} m3s_ba_reuse;
+int m3s_ba_make_plan_reuse(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                           const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                           const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                           const m3s_ba_reuse* reuse, void* workspace, size_t workspace_bytes, m3s_ba_plan* plan,
+                           void* stream);
+int m3s_ba_make_plan_kf_reuse(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp, int N,
+                              const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                              const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                              const m3s_ba_reuse* reuse, void* workspace, size_t workspace_bytes, m3s_ba_plan* plan,
+                              void* stream);
+/* packed_edges: shard edges the plan's pack wrote; changed_keyframes: keyframes found changed (all without reuse) */
+int m3s_ba_reuse_info(const m3s_ba_plan* plan, int* packed_edges, int* changed_keyframes);
+int m3s_ba_reuse_release(const void* workspace);
 int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count);
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);

@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/m3s.h"
@@ -38,6 +39,7 @@ hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, i
 int m3s_track_max_parts(void);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
+hipError_t m3s_launch_ba_kf_compare(const BaKfCopy*, int, int, uint8_t*, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, hipStream_t);
 hipError_t m3s_launch_ba_solve_dense(const BaArgs*, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
@@ -481,6 +483,7 @@ struct BaPlanImpl {
   size_t edge_sums_off, edge_sums_bytes;
   void* ws;
   unsigned long long sym_gen;  // the PlanSym (symbolic half) this plan owns, by generation
+  int n_packed, n_dirty;       // edges the pack wrote, keyframes found changed (record reuse; all without it)
 };
 static_assert(sizeof(BaPlanImpl) <= sizeof(m3s_ba_plan), "m3s_ba_plan too small");
 
@@ -512,7 +515,7 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_BLOB_SECTIONS = 20;
+constexpr int BA_BLOB_SECTIONS = 22;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
 inline size_t ba_max_pairs(int Kp) {
@@ -524,7 +527,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
   // ranks, perm, col_ptr, rowL, lev_ptr, lev_col, grp_ptr, grp, pull_grp, src, sidx, asm CSR, rhs CSR
   const size_t ints = 2 * (size_t)E + nb + (nb + 1) + nLm + (nb + 1) + nb + (nb + 2) + 4 * nLm + nb + 4 * nLm +
                       ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E +
-                      (size_t)E * chunks;  // + the linearisation block table
+                      (size_t)E * chunks +  // + the linearisation block table
+                      2 * (size_t)E;        // + record slots and the pack list (record reuse)
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -566,6 +570,50 @@ PlanStage& plan_stage() {
   std::lock_guard<std::mutex> lock(map_mu);
   return stages[dev];  // std::map nodes never move
 }
+
+// Record reuse across plans on one workspace (m3s_ba_make_plan_reuse). The backend solves once per new keyframe
+// (main.py:150-155): the edge set only grows and tracking changes only the keyframes it fuses into, so most edges'
+// point records are still valid in the workspace. Per workspace: the record slot of every directed edge (by the
+// caller's edge uid), a copy of every keyframe's points and confidences as last packed (by keyframe uid) for the
+// next plan's exact compare, and the parameters the records depend on besides those.
+struct RecCache {
+  bool valid = false;
+  int N = 0, mode = -1, W = 0;
+  float Q_thresh = 0.0f, C_thresh = 0.0f;
+  std::unordered_map<int64_t, int> slot_of;  // edge uid -> record slot (shard-local)
+  std::unordered_map<int64_t, int> copy_of;  // keyframe uid -> copy index
+  std::vector<uint32_t> scale;               // per copy: bits of the Cscale its records were packed with
+  float* copies = nullptr;                   // device: cap x 4N floats (X then C)
+  int cap = 0, used = 0;
+  BaKfCopy* table = nullptr;                 // device: tcap entries
+  BaKfCopy* table_h = nullptr;               // pinned host staging of the table
+  uint8_t* dirty = nullptr;                  // device: tcap flags
+  uint8_t* dirty_h = nullptr;                // pinned host: tcap flags
+  int tcap = 0;
+  void reset_maps() {
+    slot_of.clear();
+    copy_of.clear();
+    scale.clear();
+    used = 0;
+  }
+  void free_all() {
+    if (copies) (void)hipFree(copies);
+    if (table) (void)hipFree(table);
+    if (dirty) (void)hipFree(dirty);
+    if (table_h) (void)hipHostFree(table_h);
+    if (dirty_h) (void)hipHostFree(dirty_h);
+    copies = nullptr;
+    table = nullptr;
+    dirty = nullptr;
+    table_h = nullptr;
+    dirty_h = nullptr;
+    cap = tcap = 0;
+    reset_maps();
+    valid = false;
+  }
+};
+std::mutex g_rec_mu;
+std::map<const void*, RecCache> g_rec;  // by workspace (map nodes never move)
 
 }  // namespace
 
@@ -772,7 +820,8 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
 int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* Xh, const float* const* Ch,
                       const float* scale_h, int Kp, int N, const int64_t* ii, const int64_t* jj, int E, int e0, int e1,
                       const int64_t* idx, const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
-                      void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+                      const int64_t* edge_uid, const int64_t* kf_uid, void* workspace, size_t workspace_bytes,
+                      m3s_ba_plan* plan, void* stream) {
   M3S_CHECK(cfg && plan, "ba: null argument");
   M3S_CHECK(cfg->mode >= 0 && cfg->mode <= 2, "ba: mode must be 0 (points), 1 (rays) or 2 (calib)");
   M3S_CHECK(Kp >= 1 && N >= 1 && E >= 0, "ba: bad sizes");
@@ -802,13 +851,94 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     Y->gen = ++g_sym_gen;
     P.sym_gen = Y->gen;
   }
+  // record reuse: which keyframes changed since the workspace's previous plan (exact device compare, its flags read
+  // back with ii / jj below, no extra sync)
+  RecCache* RC = nullptr;
+  std::vector<uint8_t> kdirty(Kp, 1);
+  {
+    std::lock_guard<std::mutex> lock(g_rec_mu);
+    if (edge_uid && kf_uid) {
+      RC = &g_rec[workspace];
+    } else {
+      auto it = g_rec.find(workspace);  // a plain plan repacks every slot: whatever was cached there is gone
+      if (it != g_rec.end()) it->second.valid = false;
+    }
+  }
+  if (RC) {
+    const bool same = RC->valid && RC->N == N && RC->mode == cfg->mode && RC->Q_thresh == cfg->Q_thresh &&
+                      RC->C_thresh == cfg->C_thresh && (cfg->mode != 2 || RC->W == cfg->width);
+    if (!same) {
+      RC->reset_maps();
+      RC->N = N;
+      RC->mode = cfg->mode;
+      RC->Q_thresh = cfg->Q_thresh;
+      RC->C_thresh = cfg->C_thresh;
+      RC->W = cfg->width;
+    }
+    RC->valid = false;  // until this plan is complete
+    std::vector<int> ci(Kp, -1);
+    int fresh = 0;
+    for (int k = 0; k < Kp; k++) fresh += RC->copy_of.count(kf_uid[k]) ? 0 : 1;
+    const size_t per = (size_t)4 * N;  // floats per keyframe copy
+    if (RC->used + fresh > RC->cap) {  // grow the copies (geometric), keeping the ones in use
+      const int cap = std::max(RC->used + fresh, RC->cap + RC->cap / 2 + 8);
+      float* nc = nullptr;
+      HIP_TRY(hipStreamSynchronize(s), "ba sync");
+      HIP_TRY(hipMalloc((void**)&nc, sizeof(float) * per * cap), "ba keyframe copies");
+      if (RC->used) HIP_TRY(hipMemcpy(nc, RC->copies, sizeof(float) * per * RC->used, hipMemcpyDeviceToDevice),
+                            "ba keyframe copies");
+      if (RC->copies) (void)hipFree(RC->copies);
+      RC->copies = nc;
+      RC->cap = cap;
+    }
+    if (Kp > RC->tcap) {
+      HIP_TRY(hipStreamSynchronize(s), "ba sync");
+      if (RC->table) (void)hipFree(RC->table);
+      if (RC->dirty) (void)hipFree(RC->dirty);
+      if (RC->table_h) (void)hipHostFree(RC->table_h);
+      if (RC->dirty_h) (void)hipHostFree(RC->dirty_h);
+      RC->table = nullptr;
+      RC->dirty = nullptr;
+      RC->table_h = nullptr;
+      RC->dirty_h = nullptr;
+      RC->tcap = 0;
+      const int tc = std::max(Kp, 64);
+      HIP_TRY(hipMalloc((void**)&RC->table, sizeof(BaKfCopy) * tc), "ba reuse table");
+      HIP_TRY(hipMalloc((void**)&RC->dirty, tc), "ba reuse flags");
+      HIP_TRY(hipHostMalloc((void**)&RC->table_h, sizeof(BaKfCopy) * tc, hipHostMallocDefault), "ba reuse table");
+      HIP_TRY(hipHostMalloc((void**)&RC->dirty_h, tc, hipHostMallocDefault), "ba reuse flags");
+      RC->tcap = tc;
+    }
+    for (int k = 0; k < Kp; k++) {
+      auto it = RC->copy_of.find(kf_uid[k]);
+      const uint32_t sb = __builtin_bit_cast(uint32_t, scale_h[k]);
+      if (it == RC->copy_of.end()) {
+        ci[k] = RC->used++;
+        RC->copy_of.emplace(kf_uid[k], ci[k]);
+        RC->scale.push_back(sb);
+      } else {
+        ci[k] = it->second;
+        for (int q = 0; q < k; q++)
+          if (ci[q] == ci[k]) return fail(M3S_EINVAL, "ba reuse: duplicate keyframe uid");
+        kdirty[k] = RC->scale[ci[k]] != sb;  // the average-confidence scale 1/N changed: its records did too
+        RC->scale[ci[k]] = sb;
+      }
+      RC->table_h[k] = BaKfCopy{Xh[k], Ch[k], RC->copies + per * ci[k]};
+    }
+    HIP_TRY(hipMemcpyAsync(RC->table, RC->table_h, sizeof(BaKfCopy) * Kp, hipMemcpyHostToDevice, s), "ba reuse table");
+    HIP_TRY(hipMemsetAsync(RC->dirty, 0, Kp, s), "ba reuse flags");
+    HIP_TRY(m3s_launch_ba_kf_compare(RC->table, Kp, N, RC->dirty, s), "ba keyframe compare launch");
+    HIP_TRY(hipMemcpyAsync(RC->dirty_h, RC->dirty, Kp, hipMemcpyDeviceToHost, s), "ba reuse flags readback");
+  }
   // rank remap (gn_kernels.cu:161-170): unique(cat(ii,jj)) sorted; searchsorted; pin = 1 for rows
   std::vector<int64_t> hii(E), hjj(E);
   if (E > 0) {
     HIP_TRY(hipMemcpyAsync(hii.data(), ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba ii readback");
     HIP_TRY(hipMemcpyAsync(hjj.data(), jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba jj readback");
-    HIP_TRY(hipStreamSynchronize(s), "ba sync");
   }
+  if (E > 0 || RC) HIP_TRY(hipStreamSynchronize(s), "ba sync");
+  if (RC)
+    for (int k = 0; k < Kp; k++) kdirty[k] |= RC->dirty_h[k];
   std::vector<int64_t> u(hii);
   u.insert(u.end(), hjj.begin(), hjj.end());
   std::sort(u.begin(), u.end());
@@ -839,6 +969,33 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     std::vector<char> seen(Kp, 0);
     for (int e = e0; e < e1; e++) P.n_targets += seen[rj[e]] ? 0 : (seen[rj[e]] = 1);
   }
+  // record slots: an edge keeps the slot of its uid when that slot is still inside this shard's record range and
+  // repacks there only if one of its keyframes changed; new edges take free slots and pack
+  const int EL = e1 - e0;
+  std::vector<int> slot, pack;
+  if (RC) {
+    slot.assign(EL, -1);
+    std::vector<char> taken(EL, 0), need(EL, 0);
+    for (int t = 0; t < EL; t++) {
+      auto it = RC->slot_of.find(edge_uid[e0 + t]);
+      if (it != RC->slot_of.end() && it->second < EL && !taken[it->second]) {
+        slot[t] = it->second;
+        taken[slot[t]] = 1;
+        need[t] = kdirty[ri[e0 + t]] || kdirty[rj[e0 + t]];
+      }
+    }
+    for (int t = 0, f = 0; t < EL; t++) {
+      if (slot[t] >= 0) continue;
+      while (taken[f]) f++;
+      slot[t] = f;
+      taken[f] = 1;
+      need[t] = 1;
+    }
+    RC->slot_of.clear();
+    for (int t = 0; t < EL; t++) RC->slot_of[edge_uid[e0 + t]] = slot[t];
+    for (int t = 0; t < EL; t++)
+      if (need[t]) pack.push_back(t);
+  }
   // the tables the pack and the linearisation read, in ONE upload ahead of the pack; the symbolic tables follow
   // in the same blob (their own upload, at the first solve)
   struct Sec {
@@ -853,6 +1010,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       {Ch, sizeof(const float*) * Kp, (const void**)&P.a.Ckf},
       {scale_h, sizeof(float) * Kp, (const void**)&P.a.Cscale},
       {lin_tab.data(), sizeof(int) * lin_tab.size(), (const void**)&P.a.lin_tab},
+      {slot.data(), sizeof(int) * slot.size(), (const void**)&P.a.rec_slot},
+      {pack.data(), sizeof(int) * pack.size(), (const void**)&P.a.pack_list},
   };
   static_assert(sizeof(secs) / sizeof(secs[0]) + 14 == BA_BLOB_SECTIONS, "blob sections");
   size_t total = 0;
@@ -882,6 +1041,10 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     if (total) HIP_TRY(hipMemcpyAsync(blob, st.buf, total, hipMemcpyHostToDevice, s), "ba upload");
     HIP_TRY(hipEventRecord(st.landed, s), "ba stage record");
     st.pending = true;
+  }
+  if (!RC) {  // every edge packs into its own slot
+    P.a.rec_slot = nullptr;
+    P.a.pack_list = nullptr;
   }
   Y->dst = static_cast<char*>(blob) + total;
   HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
@@ -918,10 +1081,14 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.a.dx = dx_out ? dx_out : P.a.dx;
   // per-call point records of this shard's edges: the matched point, its pixel and the folded validity
   // weight do not change across GN iterations (only the poses do)
+  P.n_packed = RC ? (int)pack.size() : EL;
+  P.n_dirty = 0;
+  for (int k = 0; k < Kp; k++) P.n_dirty += kdirty[k];
   {
     Span sp("ba_pack", s);
-    HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, e1 - e0, s), "ba pack launch");
+    HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, P.n_packed, s), "ba pack launch");
   }
+  if (RC) RC->valid = true;
   // the symbolic analysis of ALL E edges (every rank builds the identical system) runs on a host worker while
   // the device packs and linearises
   Y->fut = std::async(std::launch::async, build_symbolic, Y, std::move(ri), std::move(rj), E, Kp, P.a.H != nullptr,
@@ -931,10 +1098,12 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
 }
 }  // namespace
 
-extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
-                                const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
-                                const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
-                                void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+extern "C" int m3s_ba_make_plan_reuse(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp,
+                                      int N, const int64_t* ii, const int64_t* jj, int E, int e0, int e1,
+                                      const int64_t* idx, const uint8_t* valid, const float* Q, float delta_thresh,
+                                      float* dx_out, const m3s_ba_reuse* reuse, void* workspace,
+                                      size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(!reuse || (reuse->edge_uid && reuse->kf_uid), "ba reuse: null uid array");
   M3S_CHECK(Xs && Cs && Kp >= 1 && N >= 1, "ba: null Xs/Cs or bad sizes");
   std::vector<const float*> xh(Kp), ch(Kp);
   std::vector<float> sh(Kp, 1.0f);  // stacked Cs is already the average confidence
@@ -943,13 +1112,16 @@ extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const floa
     ch[k] = Cs + (size_t)k * N;
   }
   return ba_make_plan_impl(cfg, Twc, xh.data(), ch.data(), sh.data(), Kp, N, ii, jj, E, e0, e1, idx, valid, Q,
-                           delta_thresh, dx_out, workspace, workspace_bytes, plan, stream);
+                           delta_thresh, dx_out, reuse ? reuse->edge_uid : nullptr, reuse ? reuse->kf_uid : nullptr,
+                           workspace, workspace_bytes, plan, stream);
 }
 
-extern "C" int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp, int N,
-                                   const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
-                                   const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
-                                   void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+extern "C" int m3s_ba_make_plan_kf_reuse(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp,
+                                         int N, const int64_t* ii, const int64_t* jj, int E, int e0, int e1,
+                                         const int64_t* idx, const uint8_t* valid, const float* Q, float delta_thresh,
+                                         float* dx_out, const m3s_ba_reuse* reuse, void* workspace,
+                                         size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  M3S_CHECK(!reuse || (reuse->edge_uid && reuse->kf_uid), "ba reuse: null uid array");
   M3S_CHECK(kf && kf->X && kf->C && kf->N_avg && Kp >= 1 && N >= 1, "ba: null keyframe table or bad sizes");
   std::vector<float> sh(Kp);
   for (int k = 0; k < Kp; k++) {
@@ -958,7 +1130,41 @@ extern "C" int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m
     sh[k] = 1.0f / kf->N_avg[k];  // torch's C / N on a device tensor: C * float32(1/N)
   }
   return ba_make_plan_impl(cfg, Twc, kf->X, kf->C, sh.data(), Kp, N, ii, jj, E, e0, e1, idx, valid, Q, delta_thresh,
-                           dx_out, workspace, workspace_bytes, plan, stream);
+                           dx_out, reuse ? reuse->edge_uid : nullptr, reuse ? reuse->kf_uid : nullptr, workspace,
+                           workspace_bytes, plan, stream);
+}
+
+extern "C" int m3s_ba_make_plan(const m3s_ba_config* cfg, float* Twc, const float* Xs, const float* Cs, int Kp, int N,
+                                const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                                const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                                void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  return m3s_ba_make_plan_reuse(cfg, Twc, Xs, Cs, Kp, N, ii, jj, E, e0, e1, idx, valid, Q, delta_thresh, dx_out,
+                                nullptr, workspace, workspace_bytes, plan, stream);
+}
+
+extern "C" int m3s_ba_make_plan_kf(const m3s_ba_config* cfg, float* Twc, const m3s_ba_keyframes* kf, int Kp, int N,
+                                   const int64_t* ii, const int64_t* jj, int E, int e0, int e1, const int64_t* idx,
+                                   const uint8_t* valid, const float* Q, float delta_thresh, float* dx_out,
+                                   void* workspace, size_t workspace_bytes, m3s_ba_plan* plan, void* stream) {
+  return m3s_ba_make_plan_kf_reuse(cfg, Twc, kf, Kp, N, ii, jj, E, e0, e1, idx, valid, Q, delta_thresh, dx_out,
+                                   nullptr, workspace, workspace_bytes, plan, stream);
+}
+
+extern "C" int m3s_ba_reuse_info(const m3s_ba_plan* plan, int* packed_edges, int* changed_keyframes) {
+  M3S_CHECK(plan && packed_edges && changed_keyframes, "ba: null argument");
+  const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
+  *packed_edges = P->n_packed;
+  *changed_keyframes = P->n_dirty;
+  return M3S_OK;
+}
+
+extern "C" int m3s_ba_reuse_release(const void* workspace) {
+  std::lock_guard<std::mutex> lock(g_rec_mu);
+  auto it = g_rec.find(workspace);
+  if (it == g_rec.end()) return M3S_OK;
+  it->second.free_all();
+  g_rec.erase(it);
+  return M3S_OK;
 }
 
 extern "C" int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count) {

@@ -149,12 +149,15 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 //   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
 //   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
+// Only the edges of a.pack_list when the plan reuses records (m3s_ba_make_plan_reuse: the rest kept theirs), each
+// into its record slot.
 template <int MODE>
-__global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int E_local) {
+__global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack) {
   const int N = p.N;
-  const size_t total = (size_t)E_local * N;
+  const size_t total = (size_t)n_pack * N;
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
-    const int e = (int)(o / N), k = (int)(o - (size_t)e * N);
+    const int t = (int)(o / N), k = (int)(o - (size_t)t * N);
+    const int e = a.pack_list ? a.pack_list[t] : t;
     const size_t g = (size_t)(e + p.edge_offset) * N + k;
     const int ix = a.ii_rank[e], jx = a.jj_rank[e];
     const bool vm = a.valid[g] != 0;
@@ -173,8 +176,31 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
     } else {
       r = make_float4(Xi[0], Xi[1], Xi[2], sw);
     }
-    a.rec[o] = r;
+    a.rec[(size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k] = r;
   }
+}
+
+// Record reuse: keyframe k's points and confidences against the library's copy from the previous plan (exact bit
+// compare, 3N + N words), dirty[k] = 1 on any difference and the copy refreshed. One block row per keyframe.
+__global__ void __launch_bounds__(256) ba_kf_compare_kernel(const BaKfCopy* __restrict__ kf, int N, uint8_t* dirty) {
+  const int k = blockIdx.y;
+  const BaKfCopy c = kf[k];
+  const unsigned* x = reinterpret_cast<const unsigned*>(c.X);
+  const unsigned* cc = reinterpret_cast<const unsigned*>(c.C);
+  unsigned* sx = reinterpret_cast<unsigned*>(c.copy);
+  unsigned* sc = sx + (size_t)3 * N;
+  bool diff = false;
+  const size_t words = (size_t)4 * N;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
+    const bool isx = i < (size_t)3 * N;
+    const unsigned v = isx ? x[i] : cc[i - (size_t)3 * N];
+    unsigned* d = isx ? &sx[i] : &sc[i - (size_t)3 * N];
+    if (*d != v) {
+      *d = v;
+      diff = true;
+    }
+  }
+  if (__any(diff) && (threadIdx.x & 63) == 0) dirty[k] = 1;
 }
 
 template <int MODE>  // specialised per residual type: one mode's registers, not the union of three
@@ -205,7 +231,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
 #endif
-  const float4* rec = a.rec + (size_t)e * N;
+  const float4* rec = a.rec + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;
   const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
@@ -936,16 +962,23 @@ extern "C" int m3s_debug_sp_stamps(unsigned long long* out) {
 #endif
 
 // ------------------------------------------------------------------------------------------
-extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
-  if (E_local <= 0) return hipSuccess;
-  const size_t total = (size_t)E_local * p->N;
+extern "C" hipError_t m3s_launch_ba_kf_compare(const BaKfCopy* kf, int Kp, int N, uint8_t* dirty, hipStream_t s) {
+  if (Kp <= 0) return hipSuccess;
+  const unsigned bx = (unsigned)std::min<size_t>(((size_t)4 * N + 255) / 256, 64);
+  hipLaunchKernelGGL(m3s::ba_kf_compare_kernel, dim3(bx, Kp), dim3(256), 0, s, kf, N, dirty);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int n_pack, hipStream_t s) {
+  if (n_pack <= 0) return hipSuccess;
+  const size_t total = (size_t)n_pack * p->N;
   const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
   if (p->mode == BA_MODE_CALIB)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, E_local);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, n_pack);
   else if (p->mode == BA_MODE_RAYS)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, E_local);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, n_pack);
   else
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, E_local);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, n_pack);
   return hipGetLastError();
 }
 

@@ -23,6 +23,14 @@ struct BaParams {
   float z_eps;
 };
 
+// record reuse (m3s_ba_make_plan_reuse): one keyframe's current buffers and the library's copy of them from the
+// previous plan on the workspace ((3N + N) floats: X then C)
+struct BaKfCopy {
+  const float* X;
+  const float* C;
+  float* copy;
+};
+
 struct BaArgs {
   float* Twc;            // (K,8) in/out
   const float* const* Xkf;  // (K) -> (N,3) keyframe points: rows of the stacked Xs, or each keyframe's X_canon
@@ -33,7 +41,9 @@ struct BaArgs {
   const int64_t* idx;    // (E,N) global edge rows
   const uint8_t* valid;  // (E,N)
   const float* Q;        // (E,N)
-  float4* rec;           // (E_local, N) per-call point records (ba_pack): {Xi | u_t, v_t, z_i ; sqrt-weight}
+  float4* rec;           // (slots, N) point records (ba_pack): {Xi | u_t, v_t, z_i ; sqrt-weight}
+  const int* rec_slot;   // (E_local) record slot of each shard edge (record reuse across plans), or null: slot = edge
+  const int* pack_list;  // (n_pack) shard edges the pack writes (the others kept their records), or null: all
   double* partials;      // (E_local*chunks, 36)
   double* edge_sums;     // (E, 36) global edge rows; all-reduced across ranks in multi-GPU BA
   // block-sparse pose system (ba_pattern.h; analysed once per plan, factored on the device every iteration)

@@ -29,6 +29,10 @@ class BaKeyframes(ctypes.Structure):
     _fields_ = [("X", ctypes.POINTER(c_void_p)), ("C", ctypes.POINTER(c_void_p)), ("N_avg", ctypes.POINTER(c_float))]
 
 
+class BaReuse(ctypes.Structure):
+    _fields_ = [("edge_uid", c_void_p), ("kf_uid", c_void_p)]
+
+
 class BaPlan(ctypes.Structure):
     _fields_ = [("opaque", ctypes.c_ubyte * 768)]
 
@@ -80,6 +84,15 @@ _SIGS = {
     "m3s_ba_make_plan_kf": ([ctypes.POINTER(BaConfig), c_void_p, ctypes.POINTER(BaKeyframes), c_int, c_int, c_void_p,
                              c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                              c_void_p, c_size_t, ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_make_plan_reuse": ([ctypes.POINTER(BaConfig), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                                ctypes.POINTER(BaReuse), c_void_p, c_size_t, ctypes.POINTER(BaPlan), c_void_p], c_int),
+    "m3s_ba_make_plan_kf_reuse": ([ctypes.POINTER(BaConfig), c_void_p, ctypes.POINTER(BaKeyframes), c_int, c_int,
+                                   c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                                   c_void_p, ctypes.POINTER(BaReuse), c_void_p, c_size_t, ctypes.POINTER(BaPlan),
+                                   c_void_p], c_int),
+    "m3s_ba_reuse_info": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), ctypes.POINTER(c_int)], c_int),
+    "m3s_ba_reuse_release": ([c_void_p], c_int),
     "m3s_ba_edge_sums": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)], c_int),
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),

@@ -17,6 +17,7 @@ an oracle backend); the product backend is ``HipShard`` over ``libm3s.so``.
 import ctypes
 from ctypes import c_void_p
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -48,6 +49,33 @@ def ba_config(mode, cfg, K=None, height=0, width=0):
     return c
 
 
+class RecordCache:
+    """A BA workspace kept across solves so the point records of unchanged edges carry over
+    (``m3s_ba_make_plan*_reuse``): the backend solves once per new keyframe (main.py:150-155) while its edge set
+    only grows. Grown with 2x headroom as the graph grows (a doubling of the edge count); a regrown workspace starts
+    a fresh cache (one full pack, what every solve costs without reuse)."""
+
+    def __init__(self):
+        self.ws = None
+
+    def workspace(self, nbytes, device):
+        if self.ws is None or self.ws.device != device or self.ws.numel() < nbytes:
+            self.release()
+            self.ws = torch.empty(int(nbytes) * 2 + 256, dtype=torch.uint8, device=device)
+        return self.ws
+
+    def release(self):
+        if self.ws is not None:
+            _lib.check(_lib.load().m3s_ba_reuse_release(_lib.ptr(self.ws)))
+            self.ws = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # interpreter shutdown
+            pass
+
+
 class HipShard:
     """One rank's view of a sharded BA problem on its GPU (libm3s split API).
 
@@ -56,7 +84,10 @@ class HipShard:
     ``keyframes = (X_list, C_list, N_list)`` with each X (N,3), C (N or N,1) the confidence sum and N the
     fusion count (``m3s_ba_make_plan_kf``)."""
 
-    def __init__(self, cfg_struct, Twc, Xs, Cs, ii, jj, idx, valid, Q, delta_thresh, e0, e1, keyframes=None):
+    def __init__(self, cfg_struct, Twc, Xs, Cs, ii, jj, idx, valid, Q, delta_thresh, e0, e1, keyframes=None,
+                 reuse=None, cache=None):
+        """reuse = (edge_uid, kf_uid) int64 host arrays + cache (a RecordCache): pack only the edges whose records
+        are not already in the cache's workspace (bit-identical results)."""
         lib = _lib.load()
         self.lib = lib
         self.dev = Twc.device
@@ -73,24 +104,41 @@ class HipShard:
         self.Kp, self.E = Kp, E
         self.dx = torch.zeros((max(Kp - 1, 0), 7), dtype=torch.float32, device=self.dev)
         nbytes = lib.m3s_ba_workspace_size(Kp, N, E)
-        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        if reuse is not None and cache is not None:
+            self.ws = cache.workspace(nbytes, self.dev)
+            edge_uid = np.ascontiguousarray(reuse[0], dtype=np.int64)
+            kf_uid = np.ascontiguousarray(reuse[1], dtype=np.int64)
+            if edge_uid.shape != (E,) or kf_uid.shape != (Kp,):
+                raise RuntimeError(f"ba reuse: need {E} edge uids and {Kp} keyframe uids")
+            self._uids = (edge_uid, kf_uid)
+            ru = ctypes.byref(_lib.BaReuse(edge_uid.ctypes.data, kf_uid.ctypes.data))
+        else:
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            ru = None
         self.keep = (Twc, Xs, Cs, ii, jj, idx, valid, Q, keyframes)
         self.plan = _lib.BaPlan()
         self.cfg = cfg_struct
-        tail = (_lib.ptr(ii), _lib.ptr(jj), E, int(e0), int(e1), _lib.ptr(idx), _lib.ptr(valid), _lib.ptr(Q),
-                float(delta_thresh), _lib.ptr(self.dx), _lib.ptr(self.ws), self.ws.numel(), ctypes.byref(self.plan),
-                _lib.stream_ptr(self.dev))
+        head = (_lib.ptr(ii), _lib.ptr(jj), E, int(e0), int(e1), _lib.ptr(idx), _lib.ptr(valid), _lib.ptr(Q),
+                float(delta_thresh), _lib.ptr(self.dx))
+        tail = (_lib.ptr(self.ws), self.ws.numel(), ctypes.byref(self.plan), _lib.stream_ptr(self.dev))
         if Xs is None:
             kt = _lib.BaKeyframes((c_void_p * Kp)(*[x.data_ptr() for x in X_list]),
                                   (c_void_p * Kp)(*[cc.data_ptr() for cc in C_list]),
                                   (ctypes.c_float * Kp)(*[float(n) for n in N_list]))
-            _lib.check(lib.m3s_ba_make_plan_kf(ctypes.byref(cfg_struct), _lib.ptr(Twc), ctypes.byref(kt), Kp, N, *tail))
+            _lib.check(lib.m3s_ba_make_plan_kf_reuse(ctypes.byref(cfg_struct), _lib.ptr(Twc), ctypes.byref(kt), Kp, N,
+                                                     *head, ru, *tail))
         else:
-            _lib.check(lib.m3s_ba_make_plan(ctypes.byref(cfg_struct), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs), Kp, N,
-                                            *tail))
+            _lib.check(lib.m3s_ba_make_plan_reuse(ctypes.byref(cfg_struct), _lib.ptr(Twc), _lib.ptr(Xs), _lib.ptr(Cs),
+                                                  Kp, N, *head, ru, *tail))
         off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
         _lib.check(lib.m3s_ba_edge_sums(ctypes.byref(self.plan), ctypes.byref(off), ctypes.byref(cnt)))
         self.edge_sums = self.ws[off.value: off.value + cnt.value].view(torch.float64)
+
+    def reuse_info(self):
+        """(shard edges the pack wrote, keyframes found changed)."""
+        packed, changed = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.m3s_ba_reuse_info(ctypes.byref(self.plan), ctypes.byref(packed), ctypes.byref(changed)))
+        return packed.value, changed.value
 
     def linearize(self):
         _lib.check(self.lib.m3s_ba_linearize(ctypes.byref(self.plan), _lib.stream_ptr(self.dev)))
@@ -119,10 +167,12 @@ def run_sharded(shard, max_iter, group=None):
 
 
 def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter, delta_thresh, K=None, height=0,
-                         width=0, group=None, keyframes=None):
+                         width=0, group=None, keyframes=None, reuse=None, cache=None, info=None):
     """Multi-GPU drop-in for mast3r_slam_backends.gauss_newton_*: same inputs (every rank holds the
     full problem, replicated), Twc updated in place identically on every rank; returns [dx]. With
-    ``Xs=None`` the keyframe points come zero-copy from ``keyframes`` (see ``HipShard``)."""
+    ``Xs=None`` the keyframe points come zero-copy from ``keyframes`` (see ``HipShard``); with ``reuse`` and
+    ``cache`` the records of unchanged edges carry over from the previous solve (``info``, a dict, receives
+    ``packed_edges`` / ``changed_keyframes``)."""
     rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     e0, e1 = shard_range(ii.shape[0], rank, world)
@@ -130,6 +180,9 @@ def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter
     if Xs is not None:
         Xs, Cs = c(Xs), c(Cs.reshape(Xs.shape[0], -1))
     shard = HipShard(ba_config(mode, cfg, K, height, width), c(Twc), Xs, Cs, c(ii), c(jj), c(idx),
-                     c(valid.reshape(idx.shape)), c(Q.reshape(idx.shape)), delta_thresh, e0, e1, keyframes=keyframes)
+                     c(valid.reshape(idx.shape)), c(Q.reshape(idx.shape)), delta_thresh, e0, e1, keyframes=keyframes,
+                     reuse=reuse, cache=cache)
+    if info is not None:
+        info["packed_edges"], info["changed_keyframes"] = shard.reuse_info()
     run_sharded(shard, max_iter, group)
     return [shard.dx]

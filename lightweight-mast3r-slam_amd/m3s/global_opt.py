@@ -1,10 +1,13 @@
 """``FactorGraph`` with the reference surface (``/root/reference/mast3r_slam/global_opt.py:14-226``).
 
 Edge insertion (``add_factors``) batches the symmetric matches of all new edges through the fused
-HIP matcher; ``solve_GN_rays`` / ``solve_GN_calib`` call the drop-in ``mast3r_slam_backends``
-operators (single GPU) or, when ``torch.distributed`` is initialised with more than one rank, the
-edge-sharded RCCL solve of ``m3s.dist_ba`` (identical result on every rank).
+HIP matcher; ``solve_GN_rays`` / ``solve_GN_calib`` run the split BA API of ``m3s.dist_ba`` with record reuse
+across solves (only new edges and edges of changed keyframes are re-packed; bit-identical to a fresh solve) and,
+when ``torch.distributed`` is initialised with more than one rank, edge-sharded over RCCL (identical result on
+every rank). With ``reuse_records = False`` a single-GPU solve calls the drop-in ``mast3r_slam_backends``
+operators.
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -53,6 +56,11 @@ class FactorGraph:
         self.window_size = self.cfg["window_size"]
         self.K = K
         self.group = None  # torch.distributed group for the sharded solve (None = WORLD)
+        # record reuse across solves (m3s.dist_ba.RecordCache): edges are append-only here, so directed edge
+        # 2u + d (undirected edge u, direction d) names the same match data in every later solve
+        self.reuse_records = True
+        self._records = None
+        self.ba_info = {}
 
     def add_factors(self, ii, jj, min_match_frac, is_reloc=False):
         """global_opt.py:32-101."""
@@ -120,6 +128,20 @@ class FactorGraph:
     def _sharded(self):
         return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
 
+    def _reuse_kw(self, unique_kf_idx):
+        """gauss_newton_sharded keywords for record reuse ({} when disabled)."""
+        if not self.reuse_records:
+            return {}
+        from m3s.dist_ba import RecordCache
+
+        if self._records is None:
+            self._records = RecordCache()
+        u = np.arange(self.ii.numel(), dtype=np.int64)
+        edge_uid = np.concatenate([2 * u, 2 * u + 1])
+        kf_uid = unique_kf_idx.cpu().numpy().astype(np.int64)
+        self.ba_info = {}
+        return {"reuse": (edge_uid, kf_uid), "cache": self._records, "info": self.ba_info}
+
     def solve_GN_rays(self):
         """global_opt.py:123-161, with the keyframe points read in place (no torch.stack of K x N x 16 B)."""
         cfg = self.cfg
@@ -128,6 +150,7 @@ class FactorGraph:
         if unique_kf_idx.numel() <= pin:
             return
         ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
+        rk = self._reuse_kw(unique_kf_idx)
         zc = self.get_poses_keyframes(unique_kf_idx)
         if zc is not None:
             from m3s.dist_ba import gauss_newton_sharded
@@ -135,16 +158,16 @@ class FactorGraph:
             T_WCs, keyframes = zc
             gauss_newton_sharded("rays", T_WCs.data[:, 0, :], None, None, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
                                  cfg, cfg["max_iters"], cfg["delta_norm"],
-                                 group=self.group, keyframes=keyframes)
+                                 group=self.group, keyframes=keyframes, **rk)
             self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])
             return
         Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
         pose_data = T_WCs.data[:, 0, :]
-        if self._sharded():
+        if self._sharded() or rk:
             from m3s.dist_ba import gauss_newton_sharded
 
             gauss_newton_sharded("rays", pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj, cfg,
-                                 cfg["max_iters"], cfg["delta_norm"], group=self.group)
+                                 cfg["max_iters"], cfg["delta_norm"], group=self.group, **rk)
         else:
             mast3r_slam_backends.gauss_newton_rays(pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
                                                    cfg["sigma_ray"], cfg["sigma_dist"], cfg["C_conf"], cfg["Q_conf"],
@@ -165,12 +188,13 @@ class FactorGraph:
         ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
         pose_data = T_WCs.data[:, 0, :]
         height, width = img_size
-        if self._sharded():
+        rk = self._reuse_kw(unique_kf_idx)
+        if self._sharded() or rk:
             from m3s.dist_ba import gauss_newton_sharded
 
             gauss_newton_sharded("calib", pose_data, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q_ii2jj, cfg,
                                  cfg["max_iters"], cfg["delta_norm"], K=K, height=height, width=width,
-                                 group=self.group)
+                                 group=self.group, **rk)
         else:
             mast3r_slam_backends.gauss_newton_calib(pose_data, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q_ii2jj,
                                                     height, width, cfg["pixel_border"], cfg["depth_eps"],

@@ -244,3 +244,75 @@ def test_backend_replay_growing_graph_vs_fp64_truth(mode, traj, monkeypatch):
     T_fin = np.stack([kfs[k].T_WC.data.cpu().numpy()[0] for k in range(n_kf)])
     gt, t0 = S.Twc_gt.cpu().numpy(), S.Twc0.cpu().numpy()
     assert np.abs(T_fin[:, :3] - gt[:, :3]).mean() < np.abs(t0[:, :3] - gt[:, :3]).mean()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,traj", [("calib", "chess"), ("rays", "euroc")])
+def test_backend_replay_record_reuse_bit_identical(mode, traj, monkeypatch):
+    """Record reuse across solves (m3s_ba_make_plan*_reuse): the replayed backend loop (main.py:116-155) with
+    FactorGraph's default reuse must give poses bit-identical to a fresh solve of the same graph from the same
+    start after EVERY call, while packing only the new edges and the edges of keyframes that changed. Every third
+    keyframe, the previous keyframe is re-fused first (tracking's update_pointmap), so changed keyframes are
+    exercised too; the workspace regrows several times as the graph grows (a fresh cache each time)."""
+    import mast3r_slam_backends as B
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.geometry import constrain_points_to_ray
+    from m3s.global_opt import FactorGraph
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SceneReplay, chess_poses, euroc_poses, intrinsics, tum_fr1_intrinsics
+
+    calib = mode == "calib"
+    monkeypatch.setitem(config, "use_calib", calib)
+    dev = torch.device("cuda")
+    n_kf, H, W = 14, 120, 160
+    K = tum_fr1_intrinsics(H, W) if calib else intrinsics(H, W)
+    S = SceneReplay((chess_poses if traj == "chess" else euroc_poses)(n_kf), H, W, K=K, device=dev)
+    kfs = Keyframes()
+    Kd = K.to(dev)
+    fg = FactorGraph(S, kfs, K=Kd, device=dev)
+    assert fg.reuse_records
+    c = config["local_opt"]
+    packed_total, edges_total, changed_seen = 0, 0, 0
+    for idx in range(n_kf):
+        X, C = S.keyframe(idx)
+        f = Frame(idx, (H, W), T_WC=Sim3(S.Twc0[idx].view(1, 8).clone()))
+        f.K = Kd
+        f.update_pointmap(X, C)
+        kfs.append(f)
+        if idx == 0:
+            continue
+        refused = idx >= 3 and idx % 3 == 0
+        if refused:  # tracking fused a frame into the previous keyframe: its points, confidences and N change
+            Xp, Cp = S.keyframe(idx - 1)
+            kfs[idx - 1].update_pointmap(Xp * 1.001, Cp * 0.5)
+        loop = [idx - 3] if idx >= 3 else []
+        fg.add_factors(sorted(set([idx - 1] + loop)), [idx] * len(set([idx - 1] + loop)), c["min_match_frac"])
+        uniq = fg.get_unique_kf_idx()
+        Xg, T_WCs, Cg = fg.get_poses_points(uniq)
+        if calib:
+            Xg = constrain_points_to_ray((H, W), Xg, Kd)
+        ii, jj, idx2, valid, Qe = fg.prep_two_way_edges()
+        T_fresh = T_WCs.data[:, 0, :].clone().contiguous()
+        if calib:
+            B.gauss_newton_calib(T_fresh, Xg, Cg, Kd, ii, jj, idx2, valid, Qe, H, W, c["pixel_border"], c["depth_eps"],
+                                 c["sigma_pixel"], c["sigma_depth"], c["C_conf"], c["Q_conf"], c["max_iters"],
+                                 c["delta_norm"])
+            fg.solve_GN_calib()
+        else:
+            B.gauss_newton_rays(T_fresh, Xg, Cg, ii, jj, idx2, valid, Qe, c["sigma_ray"], c["sigma_dist"], c["C_conf"],
+                                c["Q_conf"], c["max_iters"], c["delta_norm"])
+            fg.solve_GN_rays()
+        got = np.stack([kfs[int(k)].T_WC.data.cpu().numpy()[0] for k in uniq.tolist()])
+        want = T_fresh.cpu().numpy()
+        pin = c["pin"]
+        assert np.array_equal(got[pin:], want[pin:]), f"after keyframe {idx}: reuse differs from a fresh solve"
+        E = ii.numel()
+        packed, changed = fg.ba_info["packed_edges"], fg.ba_info["changed_keyframes"]
+        assert packed <= E
+        packed_total += packed
+        edges_total += E
+        changed_seen += changed if refused else 0
+    print(f"record reuse {traj} {mode}: packed {packed_total} of {edges_total} edge records over {n_kf - 1} solves")
+    assert packed_total < 0.6 * edges_total
+    assert changed_seen > 0
