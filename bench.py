@@ -276,6 +276,45 @@ def bench_ba(args, rank, world, dev, leg):
             "alg_bytes": f"{BA_REC_BYTES} B record x {N} points x {n_e} edges + {BA_XJ_BYTES} B X_j x {N} points x "
                          f"{info['targets']} target keyframes + {2 * info['chunks'] + 1} x {BA_SUM_BYTES} B partial/"
                          f"edge-sum rows x {n_e} edges per launch (compulsory traffic, DESIGN.md §4)"}
+    # the backend's next solve (main.py:150-155) on the same graph after tracking re-fused the newest keyframe, with
+    # record reuse (m3s_ba_make_plan_reuse via RecordCache): only that keyframe's edges repack; the calls alternate
+    # two versions of its points, so every timed call sees it changed
+    from m3s.dist_ba import RecordCache
+
+    cache = RecordCache()
+    uids = (np.arange(E, dtype=np.int64), np.arange(args.ba_kf, dtype=np.int64))
+    Xs_b = Xs.clone()
+    Xs_b[-1] *= 1.0001
+
+    def run_reuse(X_in, iters):
+        Twc = Twc0.clone()
+        sync_all(world)
+        t0 = time.perf_counter()
+        sh = HipShard(cfg, Twc, X_in, Cs, ii, jj, idx, valid, Q, 0.0, e0, e1, reuse=uids, cache=cache)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        run_sharded(sh, iters)
+        sync_all(world)
+        return time.perf_counter() - t0, t1 - t0, sh.reuse_info(), Twc
+
+    run_reuse(Xs, args.ba_iters)  # fills the cache (every edge packs)
+    run_reuse(Xs_b, args.ba_iters)
+    r_el, r_setup, r_info = [], [], None
+    for X_in in (Xs, Xs_b):
+        a_el, a_setup, r_info, Twc_r = run_reuse(X_in, args.ba_iters)
+        r_el.append(max_over_ranks(a_el, world))
+        r_setup.append(max_over_ranks(a_setup, world))
+    Twc_fresh = Twc0.clone()
+    fresh = HipShard(cfg, Twc_fresh, Xs_b, Cs, ii, jj, idx, valid, Q, 0.0, e0, e1)
+    run_sharded(fresh, args.ba_iters)
+    torch.cuda.synchronize()
+    assert torch.equal(Twc_r, Twc_fresh), "BA: record reuse differs from a fresh solve"
+    reuse = {"ms_per_call": 1e3 * sum(r_el) / len(r_el), "ms_setup": 1e3 * sum(r_setup) / len(r_setup),
+             "packed_edges": r_info[0], "changed_keyframes": r_info[1], "shard_edges": e1 - e0,
+             "note": "the next backend solve after the newest keyframe was re-fused (its X changed), record reuse "
+                     "(m3s_ba_make_plan_reuse): only its edges repack; poses bit-identical to a fresh solve"}
+    cache.release()
+    del fresh, Xs_b
     pack_s = spans["ba_pack"] * 1e-3
     pack_bytes = n_e * N * BA_PACK_EDGE_BYTES + args.ba_kf * N * BA_PACK_KF_BYTES
     pack_pmc = pmc_entry(f"ba_pack_kernel<{1 if mode == 'rays' else 2}>",
@@ -291,7 +330,8 @@ def bench_ba(args, rank, world, dev, leg):
            "pack": {"GBps": pack_bytes / pack_s / 1e9, "frac": pack_bytes / pack_s / 1e9 / HBM_PEAK_GBS,
                     "bytes": pack_bytes, "traffic": pack_pmc["traffic_bytes"] if pack_pmc else None,
                     "note": f"once per call: {BA_PACK_EDGE_BYTES} B per point and edge + {BA_PACK_KF_BYTES} B per "
-                            f"keyframe point (compulsory)"}}
+                            f"keyframe point (compulsory)"},
+           "reuse": reuse}
     del G, idx, valid, Q, Xs, Cs, shard
     torch.cuda.empty_cache()
     return out
