@@ -62,8 +62,11 @@ for rep in range(2):
     gb = E * H * W * 45 / 1e6  # MB -> MB/ms = GB/s
     import hashlib
     twc_hash = hashlib.sha1(Twc.cpu().numpy().tobytes()).hexdigest()[:12]
+    info = (ctypes.c_int * 8)()
+    _lib.check(lib.m3s_ba_plan_info(ctypes.byref(shard.plan), info))
     print(f"rep {rep}: Twc sha1 {twc_hash} E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
-          f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}", flush=True)
+          f"alg)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}  wide steps {info[3]} of {info[2]} levels",
+          flush=True)
 
 
 if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the last factor launch
