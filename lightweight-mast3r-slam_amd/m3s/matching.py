@@ -55,6 +55,20 @@ def match_halves(X, D, idx_1_to_2_init=None):
     return _match(xp, xp + b * h * w * 3 * 4, dp, dp + b * h * w * F * 4, b, h, w, F, X.device, idx_1_to_2_init)
 
 
+# Output tensors for the NEXT call of a shape, allocated right after this call's launch (while the matcher runs
+# on the device) instead of on the host's critical path between a frame's result and the next frame's first
+# launch. Each pair is a fresh allocation handed out once: the same tensors torch.empty would give at call time.
+_SPARE = {}
+_WS_BYTES = {}
+
+
+def _outputs(dev, b, n, st):
+    pair = _SPARE.pop((dev, b, n, st.value), None)
+    if pair is None:
+        pair = (torch.empty((b, n), dtype=torch.int64, device=dev), torch.empty((b, n, 1), dtype=torch.bool, device=dev))
+    return pair
+
+
 def _match(x11, x21, d11, d21, b, h, w, F, dev, idx_1_to_2_init):
     cfg = config["matching"]
     lib = _lib.load()
@@ -66,12 +80,17 @@ def _match(x11, x21, d11, d21, b, h, w, F, dev, idx_1_to_2_init):
         if init_t.numel() != b * h * w:
             raise RuntimeError("match: idx_1_to_2_init must hold B*H*W indices")
         init = init_t.data_ptr()
-    idx = torch.empty((b, h * w), dtype=torch.int64, device=dev)
-    valid = torch.empty((b, h * w, 1), dtype=torch.bool, device=dev)
     st = _lib.stream_ptr(dev)
-    ws = _lib.workspace("match", lib.m3s_match_workspace_size(b, h, w, F), dev, st)
+    idx, valid = _outputs(dev, b, h * w, st)
+    key = (b, h, w, F)
+    nbytes = _WS_BYTES.get(key)
+    if nbytes is None:
+        nbytes = _WS_BYTES[key] = lib.m3s_match_workspace_size(b, h, w, F)
+    ws = _lib.workspace("match", nbytes, dev, st)
     _lib.check(lib.m3s_match(x11, x21, d11, d21, init, idx.data_ptr(), valid.data_ptr(), b, h, w, F,
                              int(cfg["max_iter"]), float(cfg["lambda_init"]), float(cfg["convergence_thresh"]),
                              float(cfg["dist_thresh"]), int(cfg["radius"]), int(cfg["dilation_max"]), ws.data_ptr(),
                              ws.numel(), st))
+    _SPARE[(dev, b, h * w, st.value)] = (torch.empty((b, h * w), dtype=torch.int64, device=dev),
+                               torch.empty((b, h * w, 1), dtype=torch.bool, device=dev))
     return idx, valid
