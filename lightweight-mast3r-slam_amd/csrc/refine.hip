@@ -333,7 +333,10 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
   if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
 #ifdef M3S_REFINE_BSTAMPS
   const unsigned long long nact = __popcll(__ballot(active));
-  __shared__ unsigned long long s_act[4];
+  // aliases the window (done with): a separate __shared__ array would push the block past 40 KiB of LDS and
+  // change the occupancy being measured (4 -> 3 blocks per CU)
+  unsigned long long* s_act = reinterpret_cast<unsigned long long*>(&lds[0]);
+  __syncthreads();
   if (t.lane == 0) s_act[t.wid] = nact;
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x < 8192) {

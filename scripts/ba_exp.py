@@ -81,3 +81,11 @@ if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the la
           f"back {t[3 + 2 * nlev] - t[2 + nlev]:.1f} us, tail {t[4 + 2 * nlev] - t[3 + 2 * nlev]:.1f} us, "
           f"total {t[4 + 2 * nlev]:.1f}")
     print("steps:", " ".join(f"{x:.2f}" for x in steps))
+    # back substitution: stamps only after barriers (runs of single-column levels share one), root level first
+    bs = [(buf[3 + nlev + (nlev - 1 - l)] - buf[0]) / 100.0 for l in range(nlev - 1, -1, -1)]
+    prev, segs = t[2 + nlev], []
+    for l, x in zip(range(nlev - 1, -1, -1), bs):
+        if buf[3 + nlev + (nlev - 1 - l)] != 0 and x >= prev:
+            segs.append(f"L{l}:{x - prev:.2f}")
+            prev = x
+    print("back (level: us since the previous barrier):", " ".join(segs))

@@ -39,3 +39,14 @@ slow = np.argsort(dur)[-8:]
 print("slowest blocks (block, dur us, start us, active, se, cu):",
       [(int(b), round(dur[b], 1), round(start[b], 1), int(act[b]), int(se[b]), int(cu[b])) for b in slow])
 print("corr(duration, active lanes) %.3f" % np.corrcoef(dur, act)[0, 1])
+# tile of each block (refine.hip: lb = xcd_remap(block), 32x8 tiles, 16 per row at 512 wide)
+q8, r8 = nb // 8, nb % 8
+xb = np.arange(nb) % 8
+lb = np.where(xb < r8, xb * (q8 + 1), r8 * (q8 + 1) + (xb - r8) * q8) + np.arange(nb) // 8
+tx, ty = lb % 16, lb // 16
+grid = np.zeros((64, 16))
+grid[ty, tx] = dur
+print("mean block duration by tile row band (8 tile rows = 64 px each):",
+      " ".join(f"{grid[r:r + 8].mean():.0f}" for r in range(0, 64, 8)))
+print("mean block duration by tile column (32 px each):", " ".join(f"{grid[:, c].mean():.0f}" for c in range(16)))
+print("XCD (block % 8) mean durations:", " ".join(f"{dur[xb == x].mean():.0f}" for x in range(8)))
