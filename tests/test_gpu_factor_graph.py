@@ -316,3 +316,63 @@ def test_backend_replay_record_reuse_bit_identical(mode, traj, monkeypatch):
     print(f"record reuse {traj} {mode}: packed {packed_total} of {edges_total} edge records over {n_kf - 1} solves")
     assert packed_total < 0.6 * edges_total
     assert changed_seen > 0
+
+
+@pytest.mark.gpu
+def test_record_reuse_cache_invalidation():
+    """The reuse cache of a workspace: a second reuse plan packs nothing; a plain plan on the same workspace drops
+    the cache (the next reuse plan packs every edge again); changed keyframe data repacks exactly that keyframe's
+    edges; a duplicate keyframe uid is rejected; poses always equal a fresh solve's."""
+    import ctypes
+
+    from m3s import _lib
+    from m3s.config import config
+    from m3s.dist_ba import HipShard, RecordCache, ba_config, run_sharded
+    from m3s.synthetic import make_graph, two_way
+
+    H, W = 24, 32
+    G = make_graph(n_kf=6, H=H, W=W, seed=5)
+    ii, jj, idx, valid, Q = (t.cuda().contiguous() for t in two_way(G))
+    valid, Q = valid.reshape(idx.shape).contiguous(), Q.reshape(idx.shape).contiguous()
+    Xs, Cs = G["Xs"].cuda().contiguous(), G["Cs"][..., 0].cuda().contiguous()
+    E, K = ii.shape[0], Xs.shape[0]
+    cfg = ba_config("rays", config["local_opt"])
+    cache = RecordCache()
+    uids = (np.arange(E, dtype=np.int64), np.arange(K, dtype=np.int64))
+
+    def solve(X, reuse=True):
+        T = G["Twc0"].cuda().clone()
+        sh = HipShard(cfg, T, X, Cs, ii, jj, idx, valid, Q, 0.0, 0, E, reuse=uids if reuse else None,
+                      cache=cache if reuse else None)
+        run_sharded(sh, 5)
+        return T.cpu().numpy(), (sh.reuse_info() if reuse else None)
+
+    T_fresh, _ = solve(Xs, reuse=False)
+    T1, info1 = solve(Xs)
+    assert info1 == (E, K) and np.array_equal(T1, T_fresh)
+    T2, info2 = solve(Xs)
+    assert info2 == (0, 0) and np.array_equal(T2, T_fresh)
+    # a plain plan on the cache's own workspace drops the cache
+    lib = _lib.load()
+    plan = _lib.BaPlan()
+    dx = torch.zeros((K - 1, 7), dtype=torch.float32, device="cuda")
+    Tp = G["Twc0"].cuda().clone()
+    _lib.check(lib.m3s_ba_make_plan(ctypes.byref(cfg), _lib.ptr(Tp), _lib.ptr(Xs), _lib.ptr(Cs), K, H * W,
+                                    _lib.ptr(ii), _lib.ptr(jj), E, 0, E, _lib.ptr(idx), _lib.ptr(valid), _lib.ptr(Q),
+                                    0.0, _lib.ptr(dx), _lib.ptr(cache.ws), cache.ws.numel(), ctypes.byref(plan),
+                                    _lib.stream_ptr(torch.device("cuda"))))
+    torch.cuda.synchronize()
+    T3, info3 = solve(Xs)
+    assert info3[0] == E and np.array_equal(T3, T_fresh)
+    # keyframe 2 changed: exactly its edges repack, and the result is the fresh solve of the changed data
+    X2 = Xs.clone()
+    X2[2] *= 1.001
+    T_fresh2, _ = solve(X2, reuse=False)
+    T4, info4 = solve(X2)
+    n2 = int(((ii == 2) | (jj == 2)).sum())
+    assert info4 == (n2, 1) and np.array_equal(T4, T_fresh2)
+    # duplicate keyframe uids are rejected
+    bad = (uids[0], np.zeros(K, dtype=np.int64))
+    with pytest.raises(RuntimeError):
+        HipShard(cfg, G["Twc0"].cuda().clone(), Xs, Cs, ii, jj, idx, valid, Q, 0.0, 0, E, reuse=bad, cache=cache)
+    cache.release()
