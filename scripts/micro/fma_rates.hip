@@ -61,6 +61,12 @@ KERNEL(k_add_f16_sdwa_s1, unsigned, "v_add_f16_sdwa %0, %0, %1 dst_sel:WORD_0 ds
 KERNEL(k_add_f16_sdwa_d1, unsigned, "v_add_f16_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1")
 KERNEL(k_pack_b32_f16, unsigned, "v_pack_b32_f16 %0, %0, %1")
 KERNEL(k_add_f32_e64, float, "v_add_f32_e64 %0, %0, %1")
+// the odd-channel add of a half-sum chain as a 3-operand f16 op reading the high half (VOP3 op_sel), the
+// multiplier an inline 1.0: s = fma(p.hi, 1.0, s) (v_add_f16_e64 takes no op_sel on gfx950)
+KERNEL(k_fma_f16_hi1, unsigned, "v_fma_f16 %0, %1, 1.0, %0 op_sel:[1,0,0,0]")
+KERNEL(k_mad_f16_hi1, unsigned, "v_mad_f16 %0, %1, 1.0, %0 op_sel:[1,0,0,0]")
+KERNEL(k_fma_f16_v3, unsigned, "v_fma_f16 %0, %1, %1, %0")
+KERNEL(k_pk_add_f16_sel, unsigned, "v_pk_add_f16 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,1]")
 // 64-bit operands
 KERNEL(k_pk_fma_f32, double, "v_pk_fma_f32 %0, %0, %1, %1")
 KERNEL(k_pk_mul_f32, double, "v_pk_mul_f32 %0, %0, %1")
@@ -92,6 +98,8 @@ int main() {
       {"v_add_f16_e64", (const void*)k_add_f16_e64, 4}, {"v_add_f16_sdwa_s1", (const void*)k_add_f16_sdwa_s1, 4},
       {"v_add_f16_sdwa_d1", (const void*)k_add_f16_sdwa_d1, 4}, {"v_pack_b32_f16", (const void*)k_pack_b32_f16, 4},
       {"v_add_f32_e64", (const void*)k_add_f32_e64, 4},
+      {"v_fma_f16_hi1", (const void*)k_fma_f16_hi1, 4}, {"v_mad_f16_hi1", (const void*)k_mad_f16_hi1, 4},
+      {"v_fma_f16_v3", (const void*)k_fma_f16_v3, 4}, {"v_pk_add_f16_sel", (const void*)k_pk_add_f16_sel, 4},
       {"v_fma_f64", (const void*)k_fma_f64, 8},       {"v_add_f64", (const void*)k_add_f64, 8},
   };
   const int iters = 4000;
