@@ -40,7 +40,7 @@ int m3s_track_max_parts(void);
 hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_kf_compare(const BaKfCopy*, int, int, uint8_t*, hipStream_t);
-hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, hipStream_t);
+hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, const int*, const int*, hipStream_t);
 hipError_t m3s_launch_ba_solve_dense(const BaArgs*, int, int, float, hipStream_t);
 hipError_t m3s_launch_peak_fma_f32(float*, int, int, hipStream_t);
 hipError_t m3s_launch_rq_prep(const float*, int, int, int, int, int, uint4*, int, float, float*, hipStream_t);
@@ -515,7 +515,7 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_BLOB_SECTIONS = 22;
+constexpr int BA_BLOB_SECTIONS = 23;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
 inline size_t ba_max_pairs(int Kp) {
@@ -528,7 +528,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
   const size_t ints = 2 * (size_t)E + nb + (nb + 1) + nLm + (nb + 1) + nb + (nb + 2) + 4 * nLm + nb + 4 * nLm +
                       ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E +
                       (size_t)E * chunks +  // + the linearisation block table
-                      2 * (size_t)E;        // + record slots and the pack list (record reuse)
+                      2 * (size_t)E +       // + record slots and the pack list (record reuse)
+                      8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1);  // + wide-step task records
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -665,9 +666,11 @@ struct PlanSym {
   std::string err;
   // worker output (read by the main thread only after the join)
   std::vector<char> image;  // the tables, packed at 16-B aligned offsets, as uploaded
-  size_t off[14] = {0};
+  size_t off[15] = {0};
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, plan_lo_off = 0, plan_bytes = 0;
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
+  int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
+  int step_na[BA_MAX_WIDE_STEPS] = {0};    // its factor tasks (update groups follow)
   char* dst = nullptr;  // device destination (the blob region after the plan's own tables)
 };
 std::mutex g_sym_mu;
@@ -683,10 +686,29 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     Y->err = "ba: factor pattern too dense for the plan tables";
     return M3S_EINVAL;
   }
-  const std::vector<int>* secs[14] = {&S.perm, &S.col_ptr, &S.rowL, &S.lev_ptr, &S.lev_col, &S.grp_ptr, &S.grp,
-                                      &S.pull_grp, &S.src, &S.sidx, &S.asm_ptr, &S.asm_ent, &S.rhs_ptr, &S.rhs_ent};
+  // the wide steps' task records (ba_sparse_step_kernel): per task {j, b0, b1, pull group or -1} and its group's
+  // source range, so a launched task starts with its column's own loads
+  std::vector<int> step_rec;
+  {
+    const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
+    auto put = [&](int j, int g) {
+      const int* gq = g >= 0 ? &S.grp[4 * (size_t)g] : nullptr;
+      const int r[8] = {j, S.col_ptr[j], S.col_ptr[j + 1], g, gq ? gq[1] : 0, gq ? gq[2] : 0, 0, 0};
+      step_rec.insert(step_rec.end(), r, r + 8);
+    };
+    for (int l = 0; l < lmax; l++) {
+      Y->step_base[l] = (int)step_rec.size() / 8;
+      Y->step_na[l] = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
+      for (int c = l < S.nlev ? S.lev_ptr[l] : 0; c < (l < S.nlev ? S.lev_ptr[l + 1] : 0); c++)
+        put(S.lev_col[c], S.pull_grp[S.lev_col[c]]);
+      for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
+    }
+  }
+  const std::vector<int>* secs[15] = {&S.perm,    &S.col_ptr, &S.rowL,    &S.lev_ptr, &S.lev_col,
+                                      &S.grp_ptr, &S.grp,     &S.pull_grp, &S.src,    &S.sidx,
+                                      &S.asm_ptr, &S.asm_ent, &S.rhs_ptr, &S.rhs_ent, &step_rec};
   size_t total = 0;
-  for (int k = 0; k < 14; k++) {
+  for (int k = 0; k < 15; k++) {
     Y->off[k] = total;
     total += (sizeof(int) * secs[k]->size() + 15) & ~(size_t)15;
   }
@@ -695,7 +717,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     return M3S_EINVAL;
   }
   Y->image.assign(total, 0);
-  for (int k = 0; k < 14; k++)
+  for (int k = 0; k < 15; k++)
     if (!secs[k]->empty()) memcpy(Y->image.data() + Y->off[k], secs[k]->data(), sizeof(int) * secs[k]->size());
   Y->nb = S.nb;
   Y->nlev = S.nlev;
@@ -802,12 +824,12 @@ PlanSym* plan_symbolic(const BaPlanImpl* P, hipStream_t s, bool upload, int* rc)
 BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   BaArgs a = P->a;
   const char* d = Y->dst;
-  const void** dst[14] = {(const void**)&a.perm, (const void**)&a.col_ptr, (const void**)&a.rowL,
+  const void** dst[15] = {(const void**)&a.perm, (const void**)&a.col_ptr, (const void**)&a.rowL,
                           (const void**)&a.lev_ptr, (const void**)&a.lev_col, (const void**)&a.grp_ptr,
                           (const void**)&a.grp, (const void**)&a.pull_grp, (const void**)&a.src,
                           (const void**)&a.sidx, (const void**)&a.asm_ptr, (const void**)&a.asm_ent,
-                          (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent};
-  for (int k = 0; k < 14; k++) *dst[k] = d + Y->off[k];
+                          (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec};
+  for (int k = 0; k < 15; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
   a.nb = Y->nb;
@@ -1013,7 +1035,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       {slot.data(), sizeof(int) * slot.size(), (const void**)&P.a.rec_slot},
       {pack.data(), sizeof(int) * pack.size(), (const void**)&P.a.pack_list},
   };
-  static_assert(sizeof(secs) / sizeof(secs[0]) + 14 == BA_BLOB_SECTIONS, "blob sections");
+  static_assert(sizeof(secs) / sizeof(secs[0]) + 15 == BA_BLOB_SECTIONS, "blob sections");
   size_t total = 0;
   for (const Sec& x : secs) total += (x.bytes + 15) & ~(size_t)15;
   const size_t capacity = ba_blob_capacity(Kp, E, chunks);
@@ -1214,7 +1236,8 @@ extern "C" int m3s_ba_solve(const m3s_ba_plan* plan, void* stream) {
   const BaArgs a = with_symbolic(P, Y);
   Span sp("ba_solve", s);
   HIP_TRY(Y->dense ? m3s_launch_ba_solve_dense(&a, P->Kp, Y->nL, P->delta_thresh, s)
-                   : m3s_launch_ba_solve(&a, P->Kp, Y->nL, P->delta_thresh, Y->step_tasks, s),
+                   : m3s_launch_ba_solve(&a, P->Kp, Y->nL, P->delta_thresh, Y->step_tasks, Y->step_base,
+                                         Y->step_na, s),
           "ba solve launch");
   return M3S_OK;
 }

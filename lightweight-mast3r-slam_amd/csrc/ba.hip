@@ -643,19 +643,18 @@ __device__ __forceinline__ double sp_ljk(const BaArgs& a, int blk, int lane) {
 // apply the sources of group g to the rows p1 = lane and p2 = lane + 64 of column j held in v1 / v2
 // (rows beyond nrow are idle). Columns of at most 64 rows (the common case) issue the next source's
 // loads before the current one is applied.
-__device__ __forceinline__ void sp_group_regs(const BaArgs& a, const SpTables& T, int g, int noff, int nrow,
+__device__ __forceinline__ void sp_group_regs(const BaArgs& a, const SpTables& T, int2 gr, int noff, int nrow,
                                               double (&v1)[8], double (&v2)[8], int lane, double* bjk) {
-  const int4 gr = T.grp[g];
-  if (gr.y >= gr.z) return;
+  if (gr.x >= gr.y) return;
   const int p1 = lane, p2 = lane + 64;
   if (nrow <= 64) {
-    int4 pl = T.src[gr.y];
+    int4 pl = T.src[gr.x];
     const double* s1 = p1 < nrow ? sp_src_addr(a, T, pl, noff, p1) : nullptr;
     double bv = sp_ljk(a, pl.x, lane);
     double x1[8];
     if (s1) ld_row(x1, s1);
-    for (int e = gr.y; e < gr.z; e++) {
-      const bool more = e + 1 < gr.z;
+    for (int e = gr.x; e < gr.y; e++) {
+      const bool more = e + 1 < gr.y;
       const double* n1 = nullptr;
       double nbv = 0.0, y1[8];
       if (more) {
@@ -674,7 +673,7 @@ __device__ __forceinline__ void sp_group_regs(const BaArgs& a, const SpTables& T
       for (int c = 0; c < 8; c++) x1[c] = y1[c];
     }
   } else {
-    for (int e = gr.y; e < gr.z; e++) {
+    for (int e = gr.x; e < gr.y; e++) {
       const int4 pl = T.src[e];
       const double* s1 = sp_src_addr(a, T, pl, noff, p1);
       const double* s2 = p2 < nrow ? sp_src_addr(a, T, pl, noff, p2) : nullptr;
@@ -695,16 +694,16 @@ __device__ __forceinline__ void sp_group_regs(const BaArgs& a, const SpTables& T
 // rows p >= 128 of column j (columns with more than 17 off-diagonal blocks), one pass of 64 rows at a
 // time: group g's sources applied, then (when inv != nullptr) the triangular solve with L_jj
 __device__ __forceinline__ void sp_rows_extra(const BaArgs& a, const SpTables& T, int j, int b0, int noff, int nrow,
-                                              int g, const double* lo, const double* inv, int lane, double* bjk) {
+                                              bool has_g, int2 gr, const double* lo, const double* inv, int lane,
+                                              double* bjk) {
   for (int base = 128; base < nrow; base += 64) {
     const int p = base + lane;
     const bool act = p < nrow;
     double v[8];
     double* tp = act ? sp_row_addr(a, b0, noff, j, p) : nullptr;
     if (act) ld_row(v, tp);
-    if (g >= 0) {
-      const int4 gr = T.grp[g];
-      for (int e = gr.y; e < gr.z; e++) {
+    if (has_g) {
+      for (int e = gr.x; e < gr.y; e++) {
         const int4 pl = T.src[e];
         const double bv = sp_ljk(a, pl.x, lane);
         const double* sp = act ? sp_src_addr(a, T, pl, noff, p) : nullptr;
@@ -733,9 +732,10 @@ __device__ __forceinline__ void sp_rows_extra(const BaArgs& a, const SpTables& T
 // p holds row p of the column; the diagonal rows' right-looking Cholesky steps are, for the rows below
 // them, the triangular solve L_ij = A_ij L_jj^-T, and for the rhs row the forward substitution
 // y_j = L_jj^-1 b_j), then the stores. Diagonal block afterwards: lower = L_jj, column 7 = 1/L_mm.
-__device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables& T, int j, int lane, double* bjk,
-                                                 int* bad) {
-  const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
+// j's blocks [b0, b1), its pull group's source range gr (has_g) come from the caller: the plan tables (factor
+// kernel) or one task record (wide steps)
+__device__ __forceinline__ void sp_factor_column_at(const BaArgs& a, const SpTables& T, int j, int b0, int b1,
+                                                    bool has_g, int2 gr, int lane, double* bjk, int* bad) {
   const int noff = b1 - b0 - 1, nrow = 7 * (noff + 1) + 1;
   const bool has1 = lane < nrow, has2 = lane + 64 < nrow;
   double v1[8], v2[8];
@@ -743,8 +743,7 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
   double* p2 = has2 ? sp_row_addr(a, b0, noff, j, lane + 64) : nullptr;
   if (has1) ld_row(v1, p1);
   if (has2) ld_row(v2, p2);
-  const int g = T.pull_grp[j];
-  if (g >= 0) sp_group_regs(a, T, g, noff, nrow, v1, v2, lane, bjk);
+  if (has_g) sp_group_regs(a, T, gr, noff, nrow, v1, v2, lane, bjk);
   bool fail = false;
   double inv[7], lo[21];
 #pragma unroll
@@ -775,14 +774,20 @@ __device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables
   }
   if (has1) st_row(p1, v1);
   if (has2) st_row(p2, v2);
-  if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, g, lo, inv, lane, bjk);
+  if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, has_g, gr, lo, inv, lane, bjk);
+}
+
+__device__ __forceinline__ void sp_factor_column(const BaArgs& a, const SpTables& T, int j, int lane, double* bjk,
+                                                 int* bad) {
+  const int g = T.pull_grp[j];
+  const int4 gq = g >= 0 ? T.grp[g] : make_int4(0, 0, 0, 0);
+  sp_factor_column_at(a, T, j, T.col_ptr[j], T.col_ptr[j + 1], g >= 0, make_int2(gq.y, gq.z), lane, bjk, bad);
 }
 
 // B. update group g (one wave): the rows of its target column take the group's sources, loaded and
 // stored once per group
-__device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables& T, int g, int lane, double* bjk) {
-  const int j = T.grp[g].x;
-  const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
+__device__ __forceinline__ void sp_update_group_at(const BaArgs& a, const SpTables& T, int j, int b0, int b1, int2 gr,
+                                                   int lane, double* bjk) {
   const int noff = b1 - b0 - 1, nrow = 7 * (noff + 1) + 1;
   const bool has1 = lane < nrow, has2 = lane + 64 < nrow;
   double v1[8], v2[8];
@@ -790,10 +795,15 @@ __device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables&
   double* p2 = has2 ? sp_row_addr(a, b0, noff, j, lane + 64) : nullptr;
   if (has1) ld_row(v1, p1);
   if (has2) ld_row(v2, p2);
-  sp_group_regs(a, T, g, noff, nrow, v1, v2, lane, bjk);
+  sp_group_regs(a, T, gr, noff, nrow, v1, v2, lane, bjk);
   if (has1) st_row(p1, v1);
   if (has2) st_row(p2, v2);
-  if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, g, nullptr, nullptr, lane, bjk);
+  if (nrow > 128) sp_rows_extra(a, T, j, b0, noff, nrow, true, gr, nullptr, nullptr, lane, bjk);
+}
+
+__device__ __forceinline__ void sp_update_group(const BaArgs& a, const SpTables& T, int g, int lane, double* bjk) {
+  const int4 gq = T.grp[g];
+  sp_update_group_at(a, T, gq.x, T.col_ptr[gq.x], T.col_ptr[gq.x + 1], make_int2(gq.y, gq.z), lane, bjk);
 }
 
 // back substitution of column j: x_j = L_jj^-T (y_j - sum_{i in struct(j)} L_ij^T x_i); X = the solution
@@ -852,16 +862,18 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
 // the same arithmetic as inside ba_sparse_factor_kernel (bit-identical factor). The launch boundary orders
 // the steps. The leaf end of a minimum-degree tree is wide (one workgroup's 16 waves took ~12 rounds per
 // step there), the root end a chain of single columns, which stays inside the one-workgroup kernel.
-__global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int l) {
-  if (*a.done) return;
+// Each task reads one 32-B record built with the plan ({j, b0, b1, pull group} and the group's source range), in
+// the same round trip as the early-exit flag: the level / column / group table lookups that used to precede the
+// column's own loads (four dependent global round trips) are gone.
+__global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int rec_base, int na) {
   __shared__ double s_red[64];
-  const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
   const int lane = threadIdx.x;
   const int task = blockIdx.x;
-  const int c0 = l < a.nlev ? T.lev_ptr[l] : 0, na = l < a.nlev ? T.lev_ptr[l + 1] - c0 : 0;
-  const int t0 = T.grp_ptr[l], nt = T.grp_ptr[l + 1] - t0;
-  if (task < na) sp_factor_column(a, T, T.lev_col[c0 + task], lane, s_red, a.bad);
-  else if (task < na + nt) sp_update_group(a, T, t0 + task - na, lane, s_red);
+  const int4 r0 = a.step_rec[2 * (rec_base + task)], r1 = a.step_rec[2 * (rec_base + task) + 1];
+  if (*a.done) return;
+  const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
+  if (task < na) sp_factor_column_at(a, T, r0.x, r0.y, r0.z, r0.w >= 0, make_int2(r1.x, r1.y), lane, s_red, a.bad);
+  else sp_update_group_at(a, T, r0.x, r0.y, r0.z, make_int2(r1.x, r1.y), lane, s_red);
 }
 
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
@@ -996,11 +1008,15 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 }
 
 // assembly (nL factor blocks + nb rhs rows), then the one-workgroup factor / solve / retraction
+// step_tasks / step_base / step_na: per wide step its tasks, its first task record, its factor tasks (the rest are
+// update groups)
 extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, const int* step_tasks,
-                                          hipStream_t s) {
+                                          const int* step_base, const int* step_na, hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
   for (int l = 0; l < a->wide_steps; l++)
-    if (step_tasks[l] > 0) hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, l);
+    if (step_tasks[l] > 0)
+      hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],
+                         step_na[l]);
   if (((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 <= (size_t)m3s::SP_PLAN_BYTES)
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else
