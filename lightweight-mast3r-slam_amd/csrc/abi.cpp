@@ -515,7 +515,8 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_BLOB_SECTIONS = 23;
+constexpr int BA_SYM_SECTIONS = 16;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
 inline size_t ba_max_pairs(int Kp) {
@@ -529,7 +530,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       ba_max_pairs(Kp) + (nLm + 1) + 4 * (size_t)E + (nb + 1) + 2 * (size_t)E +
                       (size_t)E * chunks +  // + the linearisation block table
                       2 * (size_t)E +       // + record slots and the pack list (record reuse)
-                      8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1);  // + wide-step task records
+                      8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + wide-step task records
+                      2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm);  // + the dataflow schedule
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -666,8 +668,8 @@ struct PlanSym {
   std::string err;
   // worker output (read by the main thread only after the join)
   std::vector<char> image;  // the tables, packed at 16-B aligned offsets, as uploaded
-  size_t off[15] = {0};
-  int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, plan_lo_off = 0, plan_bytes = 0;
+  size_t off[BA_SYM_SECTIONS] = {0};
+  int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
   int step_na[BA_MAX_WIDE_STEPS] = {0};    // its factor tasks (update groups follow)
@@ -704,26 +706,6 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
       for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
     }
   }
-  const std::vector<int>* secs[15] = {&S.perm,    &S.col_ptr, &S.rowL,    &S.lev_ptr, &S.lev_col,
-                                      &S.grp_ptr, &S.grp,     &S.pull_grp, &S.src,    &S.sidx,
-                                      &S.asm_ptr, &S.asm_ent, &S.rhs_ptr, &S.rhs_ent, &step_rec};
-  size_t total = 0;
-  for (int k = 0; k < 15; k++) {
-    Y->off[k] = total;
-    total += (sizeof(int) * secs[k]->size() + 15) & ~(size_t)15;
-  }
-  if (total > capacity) {
-    Y->err = "ba: factor pattern too dense for the plan tables";
-    return M3S_EINVAL;
-  }
-  Y->image.assign(total, 0);
-  for (int k = 0; k < 15; k++)
-    if (!secs[k]->empty()) memcpy(Y->image.data() + Y->off[k], secs[k]->data(), sizeof(int) * secs[k]->size());
-  Y->nb = S.nb;
-  Y->nlev = S.nlev;
-  Y->nL = S.nL;
-  Y->plan_lo_off = (int)Y->off[1];  // col_ptr .. sidx, staged into LDS by the factor kernel
-  Y->plan_bytes = (int)(Y->off[9] + S.sidx.size() * sizeof(int) - Y->off[1]);
   // sparse or dense factorisation: measured on MI355X (scripts/ba_exp.py), the one-workgroup sparse
   // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
   // update volume); the dense one ~2.7 us per pose (its pivot chain)
@@ -765,6 +747,35 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     }
     Y->wide_steps = best_L;
   }
+  // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h); M3S_BA_FLOW=0 (A/B
+  // experiments): none, the level-synchronous loops run instead
+  std::vector<int> sched;
+  {
+    const char* f = getenv("M3S_BA_FLOW");
+    if (!(f && !strcmp(f, "0"))) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched);
+  }
+  Y->flow = sched.empty() ? 0 : 1;
+  const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
+                                                   &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
+                                                   &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
+                                                   &step_rec};
+  size_t total = 0;
+  for (int k = 0; k < BA_SYM_SECTIONS; k++) {
+    Y->off[k] = total;
+    total += (sizeof(int) * secs[k]->size() + 15) & ~(size_t)15;
+  }
+  if (total > capacity) {
+    Y->err = "ba: factor pattern too dense for the plan tables";
+    return M3S_EINVAL;
+  }
+  Y->image.assign(total, 0);
+  for (int k = 0; k < BA_SYM_SECTIONS; k++)
+    if (!secs[k]->empty()) memcpy(Y->image.data() + Y->off[k], secs[k]->data(), sizeof(int) * secs[k]->size());
+  Y->nb = S.nb;
+  Y->nlev = S.nlev;
+  Y->nL = S.nL;
+  Y->plan_lo_off = (int)Y->off[1];  // col_ptr .. sidx and the dataflow schedule, staged into LDS by the factor kernel
+  Y->plan_bytes = (int)(Y->off[10] + sched.size() * sizeof(int) - Y->off[1]);
   return M3S_OK;
 }
 
@@ -824,17 +835,18 @@ PlanSym* plan_symbolic(const BaPlanImpl* P, hipStream_t s, bool upload, int* rc)
 BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   BaArgs a = P->a;
   const char* d = Y->dst;
-  const void** dst[15] = {(const void**)&a.perm, (const void**)&a.col_ptr, (const void**)&a.rowL,
-                          (const void**)&a.lev_ptr, (const void**)&a.lev_col, (const void**)&a.grp_ptr,
-                          (const void**)&a.grp, (const void**)&a.pull_grp, (const void**)&a.src,
-                          (const void**)&a.sidx, (const void**)&a.asm_ptr, (const void**)&a.asm_ent,
-                          (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec};
-  for (int k = 0; k < 15; k++) *dst[k] = d + Y->off[k];
+  const void** dst[BA_SYM_SECTIONS] = {
+      (const void**)&a.perm,    (const void**)&a.col_ptr, (const void**)&a.rowL,    (const void**)&a.lev_ptr,
+      (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
+      (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
+      (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec};
+  for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
   a.nb = Y->nb;
   a.nlev = Y->nlev;
   a.wide_steps = Y->wide_steps;
+  a.flow = Y->flow;
   return a;
 }
 
@@ -1035,7 +1047,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       {slot.data(), sizeof(int) * slot.size(), (const void**)&P.a.rec_slot},
       {pack.data(), sizeof(int) * pack.size(), (const void**)&P.a.pack_list},
   };
-  static_assert(sizeof(secs) / sizeof(secs[0]) + 15 == BA_BLOB_SECTIONS, "blob sections");
+  static_assert(sizeof(secs) / sizeof(secs[0]) + BA_SYM_SECTIONS == BA_BLOB_SECTIONS, "blob sections");
   size_t total = 0;
   for (const Sec& x : secs) total += (x.bytes + 15) & ~(size_t)15;
   const size_t capacity = ba_blob_capacity(Kp, E, chunks);

@@ -524,6 +524,7 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL) {
 }
 
 constexpr int SP_WAVES = 16;                 // waves of the factor workgroup
+static_assert(SP_WAVES == M3S_BA_SP_WAVES, "the host's schedules assume the kernel's wave count");
 constexpr int SP_PLAN_BYTES = 144 * 1024;   // LDS for the plan's loop tables and the solution x
 
 // 1/sqrt(d) for d > 0: the v_rsq_f64 estimate (~2^-22 relative) refined by ONE Newton step (~2^-44)
@@ -570,7 +571,14 @@ __device__ unsigned long long g_sp_stamps[4096];
   do {                                                                                      \
     if (lane == 0) g_sp_stamps[3000 + (k)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
+#define TST(k)                                                                                   \
+  do {                                                                                           \
+    if (lane == 0 && (k) < 2000) g_sp_stamps[1000 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define TST(k) \
+  do {         \
+  } while (0)
 #define SPST(k) \
   do {          \
   } while (0)
@@ -590,6 +598,7 @@ struct SpTables {
   const int* pull_grp;
   const int4* src;
   const int* sidx;
+  const int* sched;
 };
 
 // the loop tables at `base`: the plan's table region [plan_lo, plan_lo + plan_bytes) staged to `base` (LDS), or
@@ -606,6 +615,7 @@ __device__ __forceinline__ SpTables sp_tables(const BaArgs& a, const int* base) 
   T.pull_grp = base + (a.pull_grp - g);
   T.src = reinterpret_cast<const int4*>(base + (reinterpret_cast<const int*>(a.src) - g));
   T.sidx = base + (a.sidx - g);
+  T.sched = base + (a.sched - g);
   return T;
 }
 
@@ -857,6 +867,122 @@ __device__ __forceinline__ void sp_back_column(const BaArgs& a, const SpTables& 
   wave_sync();
 }
 
+// ---- dataflow schedule (ba_pattern.h ba_flow_schedule): flags in LDS instead of a barrier per level ----
+// Producers publish with a workgroup-scope release (their global stores of factor blocks, or LDS writes of x,
+// complete first); consumers spin on an acquire load. All waves of the workgroup share one CU and its L1.
+__device__ __forceinline__ int flow_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void flow_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wait until every source column of group range gr is factored and `cnt` (when non-null) reads q; wave-uniform
+// Spins are bounded (~2^20 polls, tens of ms): a schedule that could not complete marks the factorisation failed
+// (dx = 0) instead of hanging the workgroup.
+constexpr int FLOW_MAX_SPINS = 1 << 20;
+__device__ __forceinline__ void flow_wait_task(const SpTables& T, int2 gr, const int* fac, const int* cnt, int q,
+                                               int lane, int* bad) {
+  const int ns = gr.y - gr.x;
+  for (int base = 0; base == 0 || base < ns; base += 63) {
+    const bool cs = lane < 63 && base + lane < ns;
+    const int k = cs ? T.src[gr.x + base + lane].y : 0;
+    const bool cc = lane == 63 && base == 0 && cnt != nullptr;
+    int spins = 0;
+    while (__ballot((cs && flow_ld(&fac[k]) == 0) || (cc && flow_ld(cnt) != q)) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FLOW_MAX_SPINS || *(volatile int*)bad) {  // stalled, or already failed: stop waiting
+        if (lane == 0) *bad = 1;
+        return;
+      }
+    }
+  }
+}
+
+// sp_back_column with its factor-block loads issued before the wait for x of struct(j) (flags xd); same
+// arithmetic in the same order (bit-identical x)
+__device__ __forceinline__ void sp_back_column_flow(const BaArgs& a, const SpTables& T, double* X, int* xd, int j,
+                                                    int lane, double* red, int* bad) {
+  const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
+  const int q = lane / 7, m = lane - 7 * (lane / 7);
+  const double* D = a.L + (size_t)b0 * 64;
+  double dl[8][8];
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    double row[8];
+    ld_row(row, D + r * 8);
+#pragma unroll
+    for (int c = 0; c < 8; c++) dl[r][c] = row[c];
+  }
+  const double yv = lane < 7 ? a.y[(size_t)j * 8 + lane] : 0.0;
+  // this lane's first two blocks (b0 + 1 + q, + 9), loaded ahead of the wait
+  const int bA = b0 + 1 + q, bB = bA + 9;
+  const bool hA = lane < 63 && bA < b1, hB = lane < 63 && bB < b1;
+  double LA[7], LB[7];
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    LA[r] = hA ? a.L[(size_t)bA * 64 + m + r * 8] : 0.0;
+    LB[r] = hB ? a.L[(size_t)bB * 64 + m + r * 8] : 0.0;
+  }
+  const int iA = hA ? T.rowL[bA] : 0, iB = hB ? T.rowL[bB] : 0;
+  for (int base = b0 + 1; base == b0 + 1 || base < b1; base += 64) {
+    const bool c = base + lane < b1;
+    const int i = c ? T.rowL[base + lane] : 0;
+    int spins = 0;
+    while (__ballot(c && flow_ld(&xd[i]) == 0) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FLOW_MAX_SPINS || *(volatile int*)bad) {
+        if (lane == 0) *bad = 1;
+        break;
+      }
+    }
+  }
+  double acc = 0.0;
+  if (hA) {
+    const double* xi = X + (size_t)iA * 8;
+#pragma unroll
+    for (int r = 0; r < 7; r++) acc = fma(LA[r], xi[r], acc);
+  }
+  if (hB) {
+    const double* xi = X + (size_t)iB * 8;
+#pragma unroll
+    for (int r = 0; r < 7; r++) acc = fma(LB[r], xi[r], acc);
+  }
+  if (lane < 63)
+    for (int b = bB + 9; b < b1; b += 9) {
+      const double* Lb = a.L + (size_t)b * 64 + m;
+      const double* xi = X + (size_t)T.rowL[b] * 8;
+#pragma unroll
+      for (int r = 0; r < 7; r++) acc = fma(Lb[r * 8], xi[r], acc);
+    }
+  red[lane] = acc;
+  wave_sync();
+  if (lane < 7) {
+    double sacc = yv;
+#pragma unroll
+    for (int qq = 0; qq < 9; qq++) sacc -= red[qq * 7 + lane];  // fixed order: deterministic
+    red[lane] = sacc;
+  }
+  wave_sync();
+  double z[7];
+#pragma unroll
+  for (int mm = 0; mm < 7; mm++) z[mm] = red[mm];
+  double x[7];
+#pragma unroll
+  for (int mm = 6; mm >= 0; mm--) {
+    double vv = z[mm];
+#pragma unroll
+    for (int p = mm + 1; p < 7; p++) vv = fma(-dl[p][mm], x[p], vv);
+    x[mm] = vv * dl[mm][7];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int mm = 0; mm < 7; mm++) X[(size_t)j * 8 + mm] = x[mm];
+    flow_st(&xd[j], 1);
+  }
+  wave_sync();
+}
+
 // One wide factor step l of the elimination tree (its level's factor tasks + the update groups whose sources
 // sit one level below) as a multi-workgroup launch: one wave per task, the same per-task code and therefore
 // the same arithmetic as inside ba_sparse_factor_kernel (bit-identical factor). The launch boundary orders
@@ -905,13 +1031,61 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   const int* base = LT ? static_cast<const int*>(s_plan) : g;
   double* X = LT ? reinterpret_cast<double*>(s_plan + xoff) : a.xs;
   const SpTables T = sp_tables(a, base);
+  const int nb = a.nb;
+  // dataflow flags after x: update groups landed per column, factored per column, x done per column
+  int* f_app = s_plan + xoff + 16 * nb;
+  int* f_fac = f_app + nb;
+  int* f_xd = f_fac + nb;
+  const bool flow = LT && a.flow;
+  if (flow) {
+    const int* fac_init = a.sched + 2 * (SP_WAVES + 1);
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+      f_app[i] = 0;
+      f_fac[i] = fac_init[i];
+      f_xd[i] = 0;
+    }
+  }
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   SPST(1);
+  const int nlev = a.nlev;
+  if (flow) {
+    // every wave walks its own task list (step order); a task waits only for its inputs
+    const int* S = T.sched;
+    const int2* wl = reinterpret_cast<const int2*>(S + 2 * (SP_WAVES + 1) + nb);
+    for (int t = S[w]; t < S[w + 1]; t++) {
+      const int2 tk = wl[t];
+      if (tk.x >= 0) {
+        const int j = tk.x, gp = T.pull_grp[j];
+        const int4 gq = gp >= 0 ? T.grp[gp] : make_int4(0, 0, 0, 0);
+        const int2 gr = make_int2(gq.y, gq.z);
+        flow_wait_task(T, gr, f_fac, &f_app[j], tk.y, lane, &s_bad);
+        TST(2 * t);
+        sp_factor_column_at(a, T, j, T.col_ptr[j], T.col_ptr[j + 1], gp >= 0, gr, lane, s_red[w], &s_bad);
+        if (lane == 0) flow_st(&f_fac[j], 1);
+      } else {
+        const int4 gq = T.grp[-1 - tk.x];
+        const int2 gr = make_int2(gq.y, gq.z);
+        flow_wait_task(T, gr, f_fac, &f_app[gq.x], tk.y, lane, &s_bad);
+        TST(2 * t);
+        sp_update_group_at(a, T, gq.x, T.col_ptr[gq.x], T.col_ptr[gq.x + 1], gr, lane, s_red[w]);
+        if (lane == 0) flow_st(&f_app[gq.x], tk.y + 1);
+      }
+      TST(2 * t + 1);
+      wave_sync();
+    }
+    __syncthreads();
+    SPST(2 + nlev);
+    const int* bs_ptr = S + SP_WAVES + 1;
+    const int* bs_col = S + 2 * (SP_WAVES + 1) + nb + 2 * S[SP_WAVES];
+    for (int t = bs_ptr[w]; t < bs_ptr[w + 1]; t++) {
+      sp_back_column_flow(a, T, X, f_xd, bs_col[t], lane, s_red[w], &s_bad);
+      FST(t);
+    }
+  }
   // step l: factor the columns of level l (each pulls its children's-level updates first) beside the
   // push updates of level l-1 into the columns above level l
-  const int nlev = a.nlev;
-  for (int l = a.wide_steps; l <= nlev; l++) {
+  for (int l = flow ? nlev + 1 : a.wide_steps; l <= nlev; l++) {
     const int c0 = l < nlev ? T.lev_ptr[l] : 0, na = l < nlev ? T.lev_ptr[l + 1] - c0 : 0;
     const int t0 = T.grp_ptr[l], nt = T.grp_ptr[l + 1] - t0;
     for (int task = w; task < na + nt; task += SP_WAVES) {
@@ -923,7 +1097,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   // back substitution, levels from the root down; runs of single-column levels stay on wave 0 with no
   // barrier between them (X in LDS: a wave's LDS accesses are ordered)
-  for (int l = nlev - 1; l >= 0; l--) {
+  for (int l = flow ? -1 : nlev - 1; l >= 0; l--) {
     const int c0 = T.lev_ptr[l], c1 = T.lev_ptr[l + 1];
     for (int c = c0 + w; c < c1; c += SP_WAVES) sp_back_column(a, T, X, T.lev_col[c], lane, s_red[w]);
     const bool chain = LT && c1 - c0 == 1 && l > 0 && T.lev_ptr[l] - T.lev_ptr[l - 1] == 1;
@@ -1017,8 +1191,15 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],
                          step_na[l]);
-  if (((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 <= (size_t)m3s::SP_PLAN_BYTES)
+  // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column
+  const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64;
+  if (a->flow && lds + (size_t)a->nb * 12 <= (size_t)m3s::SP_PLAN_BYTES)
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+  else if (lds <= (size_t)m3s::SP_PLAN_BYTES) {
+    BaArgs b = *a;
+    b.flow = 0;
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, b, K, nL, delta_thresh);
+  }
   else
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   return hipGetLastError();

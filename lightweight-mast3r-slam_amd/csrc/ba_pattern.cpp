@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <utility>
 
 namespace {
 
@@ -228,5 +229,115 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P,
   {
     std::vector<int> fill(rcnt.begin(), rcnt.end() - 1);
     for (size_t t = 0; t < rval.size(); t++) P->rhs_ent[fill[rrow[t]]++] = rval[t];
+  }
+}
+
+namespace {
+
+// greedy list scheduling: each task (in order) goes to the wave where it can start earliest, given its
+// dependencies' finish times (+ hop when a dependency finished on another wave)
+struct FlowSim {
+  int waves;
+  double hop;
+  std::vector<double> avail, fin;
+  std::vector<int> wave;
+  FlowSim(int w, double h) : waves(w), hop(h), avail(w, 0.0) {}
+  int place(const std::vector<int>& deps, double cost) {
+    int best_w = 0;
+    double best = 1e300;
+    for (int w = 0; w < waves; w++) {
+      double s = avail[w];
+      for (int d : deps) s = std::max(s, fin[d] + (wave[d] != w ? hop : 0.0));
+      if (s < best - 1e-12) {
+        best = s;
+        best_w = w;
+      }
+    }
+    wave.push_back(best_w);
+    fin.push_back(best + cost);
+    avail[best_w] = best + cost;
+    return best_w;
+  }
+};
+
+}  // namespace
+
+void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched) {
+  const int nb = P.nb, nlev = P.nlev;
+  sched->clear();
+  if (nb <= 0) return;
+  std::vector<int> lev(nb, 0);
+  for (int l = 0; l < nlev; l++)
+    for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) lev[P.lev_col[c]] = l;
+  auto nrow = [&](int j) { return 7 * (P.col_ptr[j + 1] - P.col_ptr[j]) + 1; };
+  auto passes = [&](int j) { return (nrow(j) + 63) / 64; };
+  // estimated task costs (us): a factor task ~1.5 + its pull group, an update group ~0.8, ~0.3 per source and
+  // 64-row pass (one wave alone on its SIMD issues one fp64 instruction per ~3.3 ns); hand-off ~0.15
+  FlowSim F(waves, 0.15);
+  std::vector<std::pair<int, int>> tasks;  // {code, q}
+  std::vector<int> fac_task(nb, -1), last_grp(nb, -1), napplied(nb, 0), deps;
+  auto src_deps = [&](int g) {
+    for (int e = P.grp[4 * (size_t)g + 1]; e < P.grp[4 * (size_t)g + 2]; e++) {
+      const int k = P.src[4 * (size_t)e + 1];
+      if (fac_task[k] >= 0) deps.push_back(fac_task[k]);
+    }
+  };
+  for (int l = std::max(0, wide); l <= nlev; l++) {
+    if (l < nlev)
+      for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
+        const int j = P.lev_col[c], g = P.pull_grp[j];
+        deps.clear();
+        if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
+        double cost = 1.5;
+        if (g >= 0) {
+          src_deps(g);
+          cost += 0.3 * (P.grp[4 * (size_t)g + 2] - P.grp[4 * (size_t)g + 1]) * passes(j);
+        }
+        fac_task[j] = (int)tasks.size();
+        tasks.push_back({j, napplied[j]});
+        F.place(deps, cost);
+      }
+    for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
+      const int j = P.grp[4 * (size_t)t];
+      deps.clear();
+      if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
+      src_deps(t);
+      last_grp[j] = (int)tasks.size();
+      tasks.push_back({-1 - t, napplied[j]++});
+      F.place(deps, 0.8 + 0.3 * (P.grp[4 * (size_t)t + 2] - P.grp[4 * (size_t)t + 1]) * passes(j));
+    }
+  }
+  // back substitution: parents first (a parent has the higher index); x_j needs x of struct(j), which the parent's
+  // own wait already covered (struct(j) \ {parent} lies in struct(parent))
+  FlowSim B(waves, 0.15);
+  std::vector<int> bcol, bwave(nb, -1), btask(nb, -1);
+  for (int j = nb - 1; j >= 0; j--) {
+    deps.clear();
+    if (P.col_ptr[j + 1] - P.col_ptr[j] > 1) deps.push_back(btask[P.rowL[P.col_ptr[j] + 1]]);
+    btask[j] = (int)bcol.size();
+    bcol.push_back(j);
+    bwave[j] = B.place(deps, 0.7 + 0.02 * (P.col_ptr[j + 1] - P.col_ptr[j]));
+  }
+  const int nt = (int)tasks.size();
+  sched->assign(2 * (waves + 1) + nb + 2 * (size_t)nt + nb, 0);
+  int* wl_ptr = sched->data();
+  int* bs_ptr = wl_ptr + waves + 1;
+  int* fac_init = bs_ptr + waves + 1;
+  int* wl_task = fac_init + nb;
+  int* bs_col = wl_task + 2 * (size_t)nt;
+  for (int k = 0; k < nb; k++) fac_init[k] = lev[k] < wide ? 1 : 0;
+  for (int w = 0, o = 0, ob = 0; w < waves; w++) {
+    wl_ptr[w] = o;
+    for (int i = 0; i < nt; i++)
+      if (F.wave[i] == w) {
+        wl_task[2 * o] = tasks[i].first;
+        wl_task[2 * o + 1] = tasks[i].second;
+        o++;
+      }
+    wl_ptr[w + 1] = o;
+    bs_ptr[w] = ob;
+    for (size_t i = 0; i < bcol.size(); i++)
+      if (B.wave[i] == w) bs_col[ob++] = bcol[i];
+    bs_ptr[w + 1] = ob;
   }
 }

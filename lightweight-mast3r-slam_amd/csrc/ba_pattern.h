@@ -44,3 +44,16 @@ struct BaPattern {
 // update source map (the plan's table capacity, < INT_MAX): past it the build stops with too_dense set, before a
 // dense large graph can exhaust host memory.
 void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P, size_t max_sidx = (size_t)1 << 30);
+
+// Dataflow schedule of the one-workgroup part of the numeric factorisation (steps [wide, nlev]) and of the whole
+// back substitution: instead of a barrier per elimination-tree level, every wave of the workgroup walks its own
+// task list and waits only on the tasks its inputs come from (flags in LDS). Lists come from a list-scheduling
+// simulation over the task graph (estimated task costs, a penalty for a cross-wave hand-off), tasks in step order
+// within every list, so the earliest unfinished task is always runnable (no deadlock). Per target column the
+// update groups still apply in step order (a per-column counter), so the factor is bit-identical to the
+// level-synchronous schedule. Layout (ints):
+//   [wl_ptr waves+1] [bs_ptr waves+1] [fac_init nb] [wl_task 2 x ntask] [bs_col nb]
+// wl_task = {code, q}: code >= 0 factors column code after q update groups landed on it; code < 0 runs update
+// group -1 - code once q earlier groups landed on its target. fac_init[k] = 1 for columns factored by the
+// multi-workgroup steps [0, wide). bs_col: back-substitution columns per wave, descending (parents first).
+void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched);

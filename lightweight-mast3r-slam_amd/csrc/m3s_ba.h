@@ -60,8 +60,10 @@ struct BaArgs {
   const int* pull_grp;    // (nb) the group a column's factor task runs first, or -1
   const int4* src;        // {block of L_jk, k, sidx offset, 0}
   const int* sidx;        // per group source, per block of column j: the source block of column k, or -1
+  const int* sched;       // dataflow schedule of the one-workgroup part + back substitution (ba_pattern.h)
+  int flow;               // sched present (else the level-synchronous loops)
   const int4* step_rec;   // per task of the wide steps, 2 x int4: {j, b0, b1, pull group or -1}, {src begin, end, 0, 0}
-  const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, staged into LDS by the factor kernel
+  const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, sched, staged into LDS by the factor kernel
   int plan_bytes;
   const int* asm_ptr;     // (nL+1) assembly CSR: edge*2 + (sign<0), edge order
   const int* asm_ent;

@@ -89,3 +89,22 @@ if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the la
             segs.append(f"L{l}:{x - prev:.2f}")
             prev = x
     print("back (level: us since the previous barrier):", " ".join(segs))
+    # dataflow build (flow schedule): per-task wait-done / end stamps of the factor lists, per-column end stamps of
+    # the back substitution; per wave the time spent waiting vs working, and the wave-0 timeline
+    info = (ctypes.c_int * 8)()
+    _lib.check(lib.m3s_ba_plan_info(ctypes.byref(shard.plan), info))
+    if os.environ.get("M3S_BA_FLOW", "1") != "0" and buf[1000] != 0:
+        ts = [(buf[1000 + k] - buf[0]) / 100.0 for k in range(2000)]
+        n = max(k for k in range(1000) if buf[1001 + 2 * k] != 0) + 1
+        f0 = t[1]
+        print(f"flow: {n} factor tasks; factor phase ends {t[2 + nlev]:.1f} us, back ends {t[3 + 2 * nlev]:.1f} us")
+        bt = [(buf[3000 + k] - buf[0]) / 100.0 for k in range(1000) if buf[3000 + k] != 0]
+        print("back columns stamped:", len(bt), "last", f"{max(bt):.1f}" if bt else "-")
+        prev = f0
+        line = []
+        for k in range(n):
+            if ts[2 * k] < prev - 0.05:  # next wave's list starts (stamps restart earlier)
+                break
+            line.append(f"{ts[2 * k] - prev:.2f}/{ts[2 * k + 1] - ts[2 * k]:.2f}")
+            prev = ts[2 * k + 1]
+        print("wave 0 tasks (wait/work us):", " ".join(line))
