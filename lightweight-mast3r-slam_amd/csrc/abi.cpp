@@ -586,6 +586,7 @@ struct RecCache {
   std::unordered_map<int64_t, int> slot_of;  // edge uid -> record slot (shard-local)
   std::unordered_map<int64_t, int> copy_of;  // keyframe uid -> copy index
   std::vector<uint32_t> scale;               // per copy: bits of the Cscale its records were packed with
+  std::vector<char> primed;                  // per copy: compared (and so filled) at least once
   float* copies = nullptr;                   // device: cap x 4N floats (X then C)
   int cap = 0, used = 0;
   BaKfCopy* table = nullptr;                 // device: tcap entries
@@ -597,6 +598,7 @@ struct RecCache {
     slot_of.clear();
     copy_of.clear();
     scale.clear();
+    primed.clear();
     used = 0;
   }
   void free_all() {
@@ -885,10 +887,11 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     Y->gen = ++g_sym_gen;
     P.sym_gen = Y->gen;
   }
-  // record reuse: which keyframes changed since the workspace's previous plan (exact device compare, its flags read
-  // back with ii / jj below, no extra sync)
+  // record reuse: which keyframes changed since the workspace's previous plan (exact device compare, after the rank
+  // remap below: only the keyframes this shard's edges touch are compared)
   RecCache* RC = nullptr;
   std::vector<uint8_t> kdirty(Kp, 1);
+  std::vector<int> rc_ci;  // record reuse: copy index of each keyframe
   {
     std::lock_guard<std::mutex> lock(g_rec_mu);
     if (edge_uid && kf_uid) {
@@ -945,24 +948,18 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     }
     for (int k = 0; k < Kp; k++) {
       auto it = RC->copy_of.find(kf_uid[k]);
-      const uint32_t sb = __builtin_bit_cast(uint32_t, scale_h[k]);
       if (it == RC->copy_of.end()) {
         ci[k] = RC->used++;
         RC->copy_of.emplace(kf_uid[k], ci[k]);
-        RC->scale.push_back(sb);
+        RC->scale.push_back(__builtin_bit_cast(uint32_t, scale_h[k]));
+        RC->primed.push_back(0);
       } else {
         ci[k] = it->second;
         for (int q = 0; q < k; q++)
           if (ci[q] == ci[k]) return fail(M3S_EINVAL, "ba reuse: duplicate keyframe uid");
-        kdirty[k] = RC->scale[ci[k]] != sb;  // the average-confidence scale 1/N changed: its records did too
-        RC->scale[ci[k]] = sb;
       }
-      RC->table_h[k] = BaKfCopy{Xh[k], Ch[k], RC->copies + per * ci[k]};
     }
-    HIP_TRY(hipMemcpyAsync(RC->table, RC->table_h, sizeof(BaKfCopy) * Kp, hipMemcpyHostToDevice, s), "ba reuse table");
-    HIP_TRY(hipMemsetAsync(RC->dirty, 0, Kp, s), "ba reuse flags");
-    HIP_TRY(m3s_launch_ba_kf_compare(RC->table, Kp, N, RC->dirty, s), "ba keyframe compare launch");
-    HIP_TRY(hipMemcpyAsync(RC->dirty_h, RC->dirty, Kp, hipMemcpyDeviceToHost, s), "ba reuse flags readback");
+    rc_ci.swap(ci);
   }
   // rank remap (gn_kernels.cu:161-170): unique(cat(ii,jj)) sorted; searchsorted; pin = 1 for rows
   std::vector<int64_t> hii(E), hjj(E);
@@ -970,9 +967,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     HIP_TRY(hipMemcpyAsync(hii.data(), ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba ii readback");
     HIP_TRY(hipMemcpyAsync(hjj.data(), jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, s), "ba jj readback");
   }
-  if (E > 0 || RC) HIP_TRY(hipStreamSynchronize(s), "ba sync");
-  if (RC)
-    for (int k = 0; k < Kp; k++) kdirty[k] |= RC->dirty_h[k];
+  if (E > 0) HIP_TRY(hipStreamSynchronize(s), "ba sync");
   std::vector<int64_t> u(hii);
   u.insert(u.end(), hjj.begin(), hjj.end());
   std::sort(u.begin(), u.end());
@@ -982,6 +977,32 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   for (int e = 0; e < E; e++) {
     ri[e] = (int)(std::lower_bound(u.begin(), u.end(), hii[e]) - u.begin());
     rj[e] = (int)(std::lower_bound(u.begin(), u.end(), hjj[e]) - u.begin());
+  }
+  if (RC) {
+    // the keyframes of this shard's edges: only their records can be reused here, so only they are compared (a
+    // sharded solve compares ~1/world of the keyframes per rank). A keyframe's scale and copy change only when it
+    // is compared; one compared for the first time is dirty whatever its copy holds.
+    std::vector<char> usedk(Kp, 0);
+    for (int e = e0; e < e1; e++) usedk[ri[e]] = usedk[rj[e]] = 1;
+    for (int k = 0; k < Kp; k++) {
+      const int c = rc_ci[k];
+      if (!usedk[k]) {
+        kdirty[k] = 0;
+        RC->table_h[k] = BaKfCopy{nullptr, nullptr, nullptr};
+        continue;
+      }
+      const uint32_t sb = __builtin_bit_cast(uint32_t, scale_h[k]);
+      kdirty[k] = !RC->primed[c] || RC->scale[c] != sb;  // the average-confidence scale 1/N changed: its records did too
+      RC->scale[c] = sb;
+      RC->primed[c] = 1;
+      RC->table_h[k] = BaKfCopy{Xh[k], Ch[k], RC->copies + (size_t)4 * N * c};
+    }
+    HIP_TRY(hipMemcpyAsync(RC->table, RC->table_h, sizeof(BaKfCopy) * Kp, hipMemcpyHostToDevice, s), "ba reuse table");
+    HIP_TRY(hipMemsetAsync(RC->dirty, 0, Kp, s), "ba reuse flags");
+    HIP_TRY(m3s_launch_ba_kf_compare(RC->table, Kp, N, RC->dirty, s), "ba keyframe compare launch");
+    HIP_TRY(hipMemcpyAsync(RC->dirty_h, RC->dirty, Kp, hipMemcpyDeviceToHost, s), "ba reuse flags readback");
+    HIP_TRY(hipStreamSynchronize(s), "ba sync");
+    for (int k = 0; k < Kp; k++) kdirty[k] |= RC->dirty_h[k];
   }
   // linearisation block table: this shard's edges grouped by target keyframe j, chunk-major within a
   // group, so consecutive blocks (dealt to one XCD by xcd_remap) read the same X_j slab

@@ -181,25 +181,38 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
 }
 
 // Record reuse: keyframe k's points and confidences against the library's copy from the previous plan (exact bit
-// compare, 3N + N words), dirty[k] = 1 on any difference and the copy refreshed. One block row per keyframe.
+// compare, 3N + N words), dirty[k] = 1 on any difference and the copy refreshed. One block row per keyframe; a
+// null entry (a keyframe no edge of this shard touches) is skipped. 16-B accesses where the buffers allow.
+__device__ __forceinline__ bool cmp_refresh(const unsigned* __restrict__ src, unsigned* __restrict__ dst, size_t n) {
+  bool diff = false;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+  if (n % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (size_t i = t0; i < n / 4; i += st) {
+      const uint4 v = s4[i], d = d4[i];
+      if (v.x != d.x || v.y != d.y || v.z != d.z || v.w != d.w) {
+        d4[i] = v;
+        diff = true;
+      }
+    }
+  } else {
+    for (size_t i = t0; i < n; i += st)
+      if (dst[i] != src[i]) {
+        dst[i] = src[i];
+        diff = true;
+      }
+  }
+  return diff;
+}
+
 __global__ void __launch_bounds__(256) ba_kf_compare_kernel(const BaKfCopy* __restrict__ kf, int N, uint8_t* dirty) {
   const int k = blockIdx.y;
   const BaKfCopy c = kf[k];
-  const unsigned* x = reinterpret_cast<const unsigned*>(c.X);
-  const unsigned* cc = reinterpret_cast<const unsigned*>(c.C);
+  if (c.copy == nullptr) return;
   unsigned* sx = reinterpret_cast<unsigned*>(c.copy);
-  unsigned* sc = sx + (size_t)3 * N;
-  bool diff = false;
-  const size_t words = (size_t)4 * N;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
-    const bool isx = i < (size_t)3 * N;
-    const unsigned v = isx ? x[i] : cc[i - (size_t)3 * N];
-    unsigned* d = isx ? &sx[i] : &sc[i - (size_t)3 * N];
-    if (*d != v) {
-      *d = v;
-      diff = true;
-    }
-  }
+  bool diff = cmp_refresh(reinterpret_cast<const unsigned*>(c.X), sx, (size_t)3 * N);
+  diff |= cmp_refresh(reinterpret_cast<const unsigned*>(c.C), sx + (size_t)3 * N, (size_t)N);
   if (__any(diff) && (threadIdx.x & 63) == 0) dirty[k] = 1;
 }
 
