@@ -24,6 +24,7 @@
 //     retraction + |dx| early-exit flag on device: no host synchronisation inside the GN loop.
 #include "m3s_common.hpp"
 #include "m3s_ba.h"
+#include "ba_pattern.h"  // BA_BS_* flags of the dataflow back-substitution lists
 
 namespace m3s {
 
@@ -915,7 +916,7 @@ __device__ __forceinline__ void flow_wait_task(const SpTables& T, int2 gr, const
 // sp_back_column with its factor-block loads issued before the wait for x of struct(j) (flags xd); same
 // arithmetic in the same order (bit-identical x)
 __device__ __forceinline__ void sp_back_column_flow(const BaArgs& a, const SpTables& T, double* X, int* xd, int j,
-                                                    int lane, double* red, int* bad) {
+                                                    bool wait, int lane, double* red, int* bad) {
   const int b0 = T.col_ptr[j], b1 = T.col_ptr[j + 1];
   const int q = lane / 7, m = lane - 7 * (lane / 7);
   const double* D = a.L + (size_t)b0 * 64;
@@ -938,7 +939,7 @@ __device__ __forceinline__ void sp_back_column_flow(const BaArgs& a, const SpTab
     LB[r] = hB ? a.L[(size_t)bB * 64 + m + r * 8] : 0.0;
   }
   const int iA = hA ? T.rowL[bA] : 0, iB = hB ? T.rowL[bB] : 0;
-  for (int base = b0 + 1; base == b0 + 1 || base < b1; base += 64) {
+  for (int base = b0 + 1; wait && (base == b0 + 1 || base < b1); base += 64) {
     const bool c = base + lane < b1;
     const int i = c ? T.rowL[base + lane] : 0;
     int spins = 0;
@@ -1092,7 +1093,8 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     const int* bs_ptr = S + SP_WAVES + 1;
     const int* bs_col = S + 2 * (SP_WAVES + 1) + nb + 2 * S[SP_WAVES];
     for (int t = bs_ptr[w]; t < bs_ptr[w + 1]; t++) {
-      sp_back_column_flow(a, T, X, f_xd, bs_col[t], lane, s_red[w], &s_bad);
+      const int code = bs_col[t];
+      sp_back_column_flow(a, T, X, f_xd, code & BA_BS_COL, (code & BA_BS_NOWAIT) == 0, lane, s_red[w], &s_bad);
       FST(t);
     }
   }

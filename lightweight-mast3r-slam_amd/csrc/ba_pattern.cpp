@@ -336,8 +336,16 @@ void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>*
       }
     wl_ptr[w + 1] = o;
     bs_ptr[w] = ob;
+    int prev = -1;
     for (size_t i = 0; i < bcol.size(); i++)
-      if (B.wave[i] == w) bs_col[ob++] = bcol[i];
+      if (B.wave[i] == w) {
+        const int j = bcol[i];
+        const bool has_p = P.col_ptr[j + 1] - P.col_ptr[j] > 1;
+        // the wave's previous column is j's parent (or j is a root): struct(j) is done, no wait
+        const bool own = !has_p || P.rowL[P.col_ptr[j] + 1] == prev;
+        bs_col[ob++] = j | (own ? BA_BS_NOWAIT : 0);
+        prev = j;
+      }
     bs_ptr[w + 1] = ob;
   }
 }

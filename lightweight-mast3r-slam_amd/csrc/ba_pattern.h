@@ -56,4 +56,9 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P,
 // wl_task = {code, q}: code >= 0 factors column code after q update groups landed on it; code < 0 runs update
 // group -1 - code once q earlier groups landed on its target. fac_init[k] = 1 for columns factored by the
 // multi-workgroup steps [0, wide). bs_col: back-substitution columns per wave, descending (parents first).
+// bs_col entries carry BA_BS_NOWAIT when the wave's previous column is the parent (or the column is a root): struct(j)
+// minus the parent lies in struct(parent), which the parent already waited for, so x_j needs no wait; the column is
+// the low 24 bits.
+#define BA_BS_NOWAIT (1 << 30)
+#define BA_BS_COL 0xFFFFFF
 void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched);

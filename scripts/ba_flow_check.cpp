@@ -130,10 +130,14 @@ int main(int argc, char** argv) {
     bool moved = false;
     for (int w = 0; w < W; w++) {
       if (pos[w] >= bs_ptr[w + 1]) continue;
-      const int j = bs_col[pos[w]];
+      const int j = bs_col[pos[w]] & BA_BS_COL;
       bool ok = true;
       for (int b = P.col_ptr[j] + 1; b < P.col_ptr[j + 1]; b++) ok = ok && xd[P.rowL[b]];
-      if (!ok) continue;
+      if (bs_col[pos[w]] & BA_BS_NOWAIT) {
+        if (!ok) return fail("no-wait column whose struct is not done", j);
+      } else if (!ok) {
+        continue;
+      }
       if (seen[j]++) return fail("column solved twice", j);
       xd[j] = 1;
       pos[w]++;
@@ -142,12 +146,13 @@ int main(int argc, char** argv) {
     }
     if (!moved) return fail("back-substitution deadlock", bdone, nb);
   }
-  int longest = 0, busiest = 0;
+  int longest = 0, busiest = 0, nowait = 0;
+  for (int t = 0; t < nb; t++) nowait += (bs_col[t] & BA_BS_NOWAIT) ? 1 : 0;
   for (int w = 0; w < W; w++) {
     busiest = std::max(busiest, wl_ptr[w + 1] - wl_ptr[w]);
     longest = std::max(longest, bs_ptr[w + 1] - bs_ptr[w]);
   }
-  printf("OK K %d E %d nlev %d wide %d tasks %d (max %d per wave) back columns %d (max %d per wave)\n", K,
-         (int)ri.size(), P.nlev, wide, nt, busiest, nb, longest);
+  printf("OK K %d E %d nlev %d wide %d tasks %d (max %d per wave) back columns %d (max %d per wave, %d without a wait)\n",
+         K, (int)ri.size(), P.nlev, wide, nt, busiest, nb, longest, nowait);
   return 0;
 }
