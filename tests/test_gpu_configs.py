@@ -121,6 +121,31 @@ def test_match_warm_start_at_c1_matches_oracle():
     assert float((g_valid.cpu().numpy() != r_valid).mean()) <= 1e-3
 
 
+def test_batched_symmetric_match_at_c3_size_matches_oracle():
+    """The factor graph's edge matching at full C2/C3 size (512x384): B = 2 n pairs, each edge in both directions
+    (FactorGraph.add_factors -> mast3r_match_symmetric, mast3r_utils.py:162-168), in ONE fused match call against
+    the oracle on the same batch (only small batched shapes were checked)."""
+    from m3s.matching import match
+    from m3s.synthetic import tum_fr1_intrinsics
+
+    H, W = 384, 512
+    Ps = [_pair(H, W, seed=s, K=tum_fr1_intrinsics(H, W)) for s in (21, 22)]
+    X11 = np.concatenate([np.stack((P["X"][0], P["X"][1])) for P in Ps])  # i->j, j->i per edge
+    X21 = np.concatenate([np.stack((P["X"][1], P["X"][0])) for P in Ps])
+    D11 = np.concatenate([np.stack((P["D"][0], P["D"][1])) for P in Ps])
+    D21 = np.concatenate([np.stack((P["D"][1], P["D"][0])) for P in Ps])
+    r_idx, r_valid = O.match(X11, X21, D11, D21)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    g_idx, g_valid = match(t(X11), t(X21), t(D11), t(D21))
+    g_idx, g_valid = g_idx.cpu().numpy(), g_valid.cpu().numpy()
+    assert g_idx.shape == (4, H * W) and g_valid.shape == (4, H * W, 1)
+    for b in range(4):
+        mis = float((g_idx[b] != r_idx[b]).mean())
+        mis_v = float((g_valid[b] != r_valid[b]).mean())
+        print(f"C3 batched match row {b}: idx mismatch {mis:.2e}, valid mismatch {mis_v:.2e}")
+        assert mis <= 1e-3 and mis_v <= 1e-3
+
+
 SIG = {"rays": (0.003, 10.0), "calib": (1.0, 10.0)}
 
 
