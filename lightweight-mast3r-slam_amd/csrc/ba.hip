@@ -94,6 +94,26 @@ __device__ __forceinline__ f2 rcp2(f2 x) {
   return y;
 }
 
+// BA_LIN_MATRIX: the per-point Sim(3) action as X + (D X + t) with the per-edge D = s R - I (3 packed FMAs + an add
+// per component instead of the quaternion expression's 12 ops under -ffp-contract=off). BA_LIN_FMA: explicit FMAs in
+// the calib rows' product-sums (pixel projection, the (1 + x^2) Jacobian terms). Measured on MI355X (scripts/
+// gpu_r03s2_i.sh, scripts/ba_acc.py): lin C5 2.20 -> 1.94 ms, C4 1.88 -> 1.80 ms; every BA fixture <= 8e-6 from the
+// fp64 truth (max: K=256 EuRoC rays 8.0e-6). FMAs in the rays rows gained 1.4 % and cost accuracy (EuRoC 8.6e-6):
+// not used.
+#ifndef BA_LIN_MATRIX
+#define BA_LIN_MATRIX 1
+#endif
+#ifndef BA_LIN_FMA
+#define BA_LIN_FMA 1
+#endif
+__device__ __forceinline__ f2 BA_FMA2(f2 a, f2 b, f2 c) {
+#if BA_LIN_FMA
+  return __builtin_elementwise_fma(a, b, c);
+#else
+  return a * b + c;
+#endif
+}
+
 // actSO3 of two points (component arrays), same expression as actSO3
 __device__ __forceinline__ void actSO3_v(const float* q, const f2* X, f2* Y) {
   const f2 uv0 = 2.0f * (q[1] * X[2] - q[2] * X[1]);
@@ -233,6 +253,27 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     Tj[c] = a.Twc[jx * 8 + c];
   }
   relSim3(Ti, Tj, Tij);
+#if BA_LIN_MATRIX
+  // the linear map of actSO3 (Y = X + 2w q x X + 2 q x (q x X), any |q|) times s, formed in fp64 once per block:
+  // s (I + 2w[q]x + 2([q][q]^T - |q|^2 I)), kept as its difference from the identity, D = s R - I (Y = X + (D X + t)):
+  // D is small for the near-identity relative poses of co-visible keyframes, so rounding it to fp32 costs far less
+  // than rounding s R itself (which put the ill-conditioned 6-KF fixtures at 1.6-1.8e-5 from the fp64 truth)
+  float M[9];
+  {
+    const double x = Tij[3], y = Tij[4], z = Tij[5], w = Tij[6], sc = Tij[7];
+    const double R[9] = {1.0 - 2.0 * (y * y + z * z), 2.0 * (x * y - z * w),       2.0 * (x * z + y * w),
+                         2.0 * (x * y + z * w),       1.0 - 2.0 * (x * x + z * z), 2.0 * (y * z - x * w),
+                         2.0 * (x * z - y * w),       2.0 * (y * z + x * w),       1.0 - 2.0 * (x * x + y * y)};
+#pragma unroll
+    for (int c = 0; c < 9; c++) {  // block-uniform: kept in SGPRs (the packed FMAs read them as scalar operands)
+      const double d = sc * R[c] - ((c % 4 == 0) ? 1.0 : 0.0);
+      M[c] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, (float)d)));
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+      Tij[c] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, Tij[c])));
+  }
+#endif
 #if BA_PAIR_ACC
   const bool odd = threadIdx.x & 1;
   double acc[BA_PAIR_HALF];
@@ -276,9 +317,20 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     // sqrt(q), 0 for an invalid match (ba_pack) and for the missing second point of a ragged tail
     const f2 sqq = {R0.w, has1 ? R1.w : 0.0f};
     f2 Y[3];
+#if BA_LIN_MATRIX
+    // actSim3 (gn_kernels.cu:207-219) as the edge's map X + (D X + t): three packed FMAs and an add per component
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+      Y[c] = Xj[c] + __builtin_elementwise_fma(
+                         f2{M[3 * c], M[3 * c]}, Xj[0],
+                         __builtin_elementwise_fma(f2{M[3 * c + 1], M[3 * c + 1]}, Xj[1],
+                                                   __builtin_elementwise_fma(f2{M[3 * c + 2], M[3 * c + 2]}, Xj[2],
+                                                                             f2{Tij[c], Tij[c]})));
+#else
     actSO3_v(&Tij[3], Xj, Y);  // actSim3 (gn_kernels.cu:207-219): rotate, scale, translate
 #pragma unroll
     for (int c = 0; c < 3; c++) Y[c] = Y[c] * Tij[7] + Tij[c];
+#endif
     if constexpr (MODE == BA_MODE_POINTS) {
       const f2 err[3] = {Y[0] - Rx, Y[1] - Ry, Y[2] - Rz};
       const f2 sw = p.inv_a * sqq;
@@ -326,7 +378,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       const f2 zj_log = valid_z ? f2{__logf(Y[2].x), __logf(Y[2].y)} : z2;
       const f2 zi_log = valid_z ? f2{__logf(zi.x), __logf(zi.y)} : z2;
       const f2 xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
-      const f2 u = p.fx * xz + p.cx, vv = p.fy * yz + p.cy;
+      const f2 u = BA_FMA2(f2{p.fx, p.fx}, xz, f2{p.cx, p.cx}), vv = BA_FMA2(f2{p.fy, p.fy}, yz, f2{p.cy, p.cy});
       const float ub = (float)p.pixel_border, uh = (float)(p.W - 1 - p.pixel_border),
                   vh = (float)(p.H - 1 - p.pixel_border);
       const auto valid = (u > ub) & (u < uh) & (vv > ub) & (vv < vh) & valid_z;
@@ -336,8 +388,8 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       const f2 wp = swp * swp, wd = swd * swd;
       const float fx = p.fx, fy = p.fy;
       const f2 o2 = {1.0f, 1.0f};
-      const f2 J0[7] = {fx * zj_inv, z2, -fx * xz * zj_inv, -fx * xz * yz, fx * (o2 + xz * xz), -fx * yz, z2};
-      const f2 J1[7] = {z2, fy * zj_inv, -fy * yz * zj_inv, -fy * (o2 + yz * yz), fy * xz * yz, fy * xz, z2};
+      const f2 J0[7] = {fx * zj_inv, z2, -fx * xz * zj_inv, -fx * xz * yz, fx * BA_FMA2(xz, xz, o2), -fx * yz, z2};
+      const f2 J1[7] = {z2, fy * zj_inv, -fy * yz * zj_inv, -fy * BA_FMA2(yz, yz, o2), fy * xz * yz, fy * xz, z2};
       const f2 J2[7] = {z2, z2, zj_inv, yz, -xz, z2, o2};
       acc_local_f2<0b0111101>(fL, fv, J0, huber_ba2(swp * err[0]) * wp, err[0]);  // {0,2,3,4,5}
       acc_local_f2<0b0111110>(fL, fv, J1, huber_ba2(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
