@@ -70,7 +70,8 @@ __device__ __forceinline__ f2 huber_ba2(f2 r) {
   const f2 q0 = KH * y;
   const f2 e = __builtin_elementwise_fma(-q0, ra, f2{KH, KH}) + KL;
   const f2 q = __builtin_elementwise_fma(e, y, q0);
-  return ra < KH ? f2{1.0f, 1.0f} : q;
+  // |r| < k -> 1, else k/|r| (<= 1): min(1, q), with |r| = 0 (q NaN from rcp(0) * 0) -> 1 by min's NaN rule
+  return f2{fminf(1.0f, q.x), fminf(1.0f, q.y)};
 }
 
 // 1/sqrt(x) and 1/x of two values: the hardware estimates (~1 ulp) refined by one Newton step each (packed), which
