@@ -206,7 +206,8 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
     (default: the plan's cost-model split; M3S_BA_WIDE=t: every step up to the last one wider than t tasks, 0: every
     step) or all steps inside one
     workgroup (M3S_BA_WIDE huge) — run the same per-task arithmetic in the same order: poses and dx must be
-    bit-identical on the K=256 chess graph."""
+    bit-identical on the K=256 chess graph. Each split runs with the one-workgroup part on its dataflow schedule
+    (default) and level-synchronous (M3S_BA_FLOW=0): the per-column update order is the same, so bit-identical too."""
     import mast3r_slam_backends as B
 
     G = chess_graph
@@ -215,14 +216,17 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
                             else torch.from_numpy(np.ascontiguousarray(a)).to(dt)).cuda()
     args = (c(G["Xs"]), c(G["Cs"]), c(G["ii"]), c(G["jj"]), c(G["idx"]), c(G["valid"], torch.bool), c(G["Q"]))
     out = {}
-    for wide in ("1000000", "16", "0", "default"):
-        if wide == "default":  # the plan's cost-model split
-            monkeypatch.delenv("M3S_BA_WIDE", raising=False)
-        else:
-            monkeypatch.setenv("M3S_BA_WIDE", wide)
-        T = c(G["Twc0"])
-        dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
-        out[wide] = (T.cpu().numpy(), dx.cpu().numpy())
-    for wide in ("16", "0", "default"):
-        assert np.array_equal(out[wide][0], out["1000000"][0]), f"poses differ with M3S_BA_WIDE={wide}"
-        assert np.array_equal(out[wide][1], out["1000000"][1]), f"dx differs with M3S_BA_WIDE={wide}"
+    for flow in ("1", "0"):
+        monkeypatch.setenv("M3S_BA_FLOW", flow)
+        for wide in ("1000000", "16", "0", "default"):
+            if wide == "default":  # the plan's cost-model split
+                monkeypatch.delenv("M3S_BA_WIDE", raising=False)
+            else:
+                monkeypatch.setenv("M3S_BA_WIDE", wide)
+            T = c(G["Twc0"])
+            dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
+            out[(flow, wide)] = (T.cpu().numpy(), dx.cpu().numpy())
+    ref = out[("0", "1000000")]
+    for key, (T, dx) in out.items():
+        assert np.array_equal(T, ref[0]), f"poses differ with M3S_BA_FLOW, M3S_BA_WIDE = {key}"
+        assert np.array_equal(dx, ref[1]), f"dx differs with M3S_BA_FLOW, M3S_BA_WIDE = {key}"
