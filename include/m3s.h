@@ -22,12 +22,15 @@
 extern "C" {
 #endif
 
-#define M3S_ABI_VERSION 4
+#define M3S_ABI_VERSION 5
 
 #define M3S_OK 0
 #define M3S_EINVAL -1  /* bad shape / argument (reference: TORCH_CHECK -> RuntimeError) */
 #define M3S_EHIP -2    /* HIP launch / runtime failure */
 #define M3S_ESPACE -3  /* workspace too small */
+#define M3S_ESTALL -4  /* global BA: a bounded dataflow hand-off wait of the factorisation timed out (a schedule
+                        * fault, not a non-positive pivot): the GN loop stopped; reported by m3s_ba_iterations and
+                        * m3s_gauss_newton. A non-positive pivot keeps the reference contract (dx = 0, no error). */
 
 int m3s_abi_version(void);
 const char* m3s_last_error(void);

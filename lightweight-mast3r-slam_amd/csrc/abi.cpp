@@ -21,17 +21,19 @@
 #include "m3s_track.h"
 
 extern "C" {
-hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, hipStream_t);
+hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, float*, int, hipStream_t);
+int m3s_refine_tile_ok(int, int, int, int, int, int);
+int m3s_prep_parts(int, int, int);
 hipError_t m3s_launch_iter_proj(const float*, const float*, const float*, float*, uint8_t*, int, int, int, int, int,
                                 float, float, hipStream_t);
 hipError_t m3s_launch_proj_occlusion(const float*, const float*, const float*, const int64_t*, int*, uint8_t*, int, int,
-                                     int, int, float, float, float, int*, hipStream_t);
+                                     int, int, float, float, float, int*, const float*, int, float*, hipStream_t);
 hipError_t m3s_launch_refine_f16(const void*, const void*, const int64_t*, int64_t*, int, int, int, int, int, int, int,
                                  hipStream_t);
 hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int64_t*, int, int, int, int, int, int,
                                  int, hipStream_t);
 hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*, int, int, int, int, int, int,
-                                 void*, int*, hipStream_t);
+                                 void*, int*, const float*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
 hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
 hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, const TrackPublish*, hipStream_t);
@@ -210,10 +212,13 @@ extern "C" int m3s_refine_matches(int dtype, const void* D11, const void* D21, c
 // ------------------------------------------------------------------------------------------
 struct MatchWs {
   float* rays9;   // (B,H,W,9) rays + gradients
-  void* D11h;     // (B,H,W,F) f16
+  void* D11h;     // f16: (B,3,H,W,8) chunk planes on the refine tile path, else (B,H,W,F)
   int* p1;        // (B,N,2) int32
   int4* olist;    // (B*N) refine deferred-outlier records
   int* ocount;    // refine deferred-outlier count
+  float* cpart;   // prep's per-block descriptor-norm maxima (the refine screen's bound)
+  float* cmax;    // their maximum (proj_occlusion reduces, refine reads)
+  int nparts;
 };
 
 static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
@@ -222,6 +227,9 @@ static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
   w->p1 = c.take<int>((size_t)B * H * W * 2);
   w->olist = c.take<int4>((size_t)B * H * W);
   w->ocount = c.take<int>(1);
+  w->nparts = m3s_prep_parts(B, H, W);
+  w->cpart = c.take<float>((size_t)w->nparts);
+  w->cmax = c.take<float>(1);
   return c.off;
 }
 
@@ -247,14 +255,23 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   void* D11h = w.D11h;
   int* p1 = w.p1;
   hipStream_t s = (hipStream_t)stream;
+  // bound-screened refine (refine.hip): prep publishes the descriptor-norm bound; M3S_REFINE_SCREEN=0 scores every
+  // candidate with the exact chain instead (same results, bit for bit; read per call so tests can compare both)
+  const char* screen_env = getenv("M3S_REFINE_SCREEN");
+  // the refine tile kernel reads prep's chunk-planar D11h (refine.hip); the per-pixel fallback the (H,W,F) one
+  const int planar = radius > 0 && m3s_refine_tile_ok(B, H, W, F, radius, dilation_max);
+  const bool screen = (screen_env == nullptr || atoi(screen_env) != 0) && planar;
   {
     Span sp("prep_rays", s);
-    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 ? D11 : nullptr, D11h, B, H, W, F, s), "match prep launch");
+    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 ? D11 : nullptr, D11h, B, H, W, F, screen ? w.cpart : nullptr,
+                            planar, s),
+            "match prep launch");
   }
   {
     Span sp("proj_occlusion", s);
     HIP_TRY(m3s_launch_proj_occlusion(rays9, X11, X21, idx_init, p1, valid_out, B, H, W, max_iter, lambda_init,
-                                      cost_thresh, dist_thresh, w.ocount, s),
+                                      cost_thresh, dist_thresh, w.ocount, w.cpart, w.nparts,
+                                      screen ? w.cmax : nullptr, s),
             "match proj launch");
   }
   // radius == 0: the refine loop is empty and the kernel only writes idx = pixel_to_lin(p1)
@@ -262,7 +279,7 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   {
     Span sp("refine_lin", s);
     HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, w.olist,
-                                  w.ocount, s),
+                                  w.ocount, screen ? w.cmax : nullptr, s),
             "match refine launch");
   }
   return M3S_OK;
@@ -548,7 +565,7 @@ size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* 
   // the dense fallback's system (graphs up to BA_DENSE_MAX_POSES poses)
   const size_t n = (size_t)nb * 7;
   a->H = Kp <= BA_DENSE_MAX_POSES ? c.take<double>(std::max<size_t>((2 * n + 1) * n, 1)) : nullptr;
-  a->info = c.take<int>(4);
+  a->info = c.take<int>(8);
   a->done = a->info + 1;
   a->iters = a->info + 2;
   *blob = c.take<char>(ba_blob_capacity(Kp, E, chunks));
@@ -1102,9 +1119,14 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     P.a.pack_list = nullptr;
   }
   Y->dst = static_cast<char*>(blob) + total;
-  HIP_TRY(hipMemsetAsync(P.a.info, 0, 4 * sizeof(int), s), "ba memset");
+  HIP_TRY(hipMemsetAsync(P.a.info, 0, 8 * sizeof(int), s), "ba memset");
   HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");
   P.a.bad = P.a.info + 3;
+  P.a.stalled = P.a.info + 4;
+  {
+    const char* e = getenv("M3S_BA_FORCE_STALL");
+    P.a.force_stall = e != nullptr && atoi(e) != 0;
+  }
   P.a.Twc = Twc;
   P.a.idx = idx;
   P.a.valid = valid;
@@ -1279,8 +1301,13 @@ extern "C" int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* 
   M3S_CHECK(plan && iters_out, "ba: null argument");
   const BaPlanImpl* P = reinterpret_cast<const BaPlanImpl*>(plan->opaque);
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemcpyAsync(iters_out, P->a.iters, sizeof(int), hipMemcpyDeviceToHost, s), "ba readback");
+  int st[3];  // iters, bad, stalled (info + 2 .. + 4)
+  HIP_TRY(hipMemcpyAsync(st, P->a.iters, sizeof(st), hipMemcpyDeviceToHost, s), "ba readback");
   HIP_TRY(hipStreamSynchronize(s), "ba sync");
+  *iters_out = st[0];
+  if (st[2] != 0)
+    return fail(M3S_ESTALL, "ba: a factor-schedule hand-off stalled (bounded wait timed out); poses were not updated "
+                            "by the stalled iteration and the loop stopped");
   return M3S_OK;
 }
 
@@ -1299,8 +1326,10 @@ extern "C" int m3s_gauss_newton(const m3s_ba_config* cfg, float* Twc, const floa
     if ((rc = m3s_ba_linearize(&plan, stream)) != M3S_OK) return rc;
     if ((rc = m3s_ba_solve(&plan, stream)) != M3S_OK) return rc;
   }
-  if (iters_out) return m3s_ba_iterations(&plan, iters_out, stream);
-  return M3S_OK;
+  // one readback per call (the reference's host loop syncs every iteration): the iteration count and the
+  // schedule-stall check (M3S_ESTALL), so a stalled solve is an error, never silently unoptimised poses
+  int iters_local = 0;
+  return m3s_ba_iterations(&plan, iters_out ? iters_out : &iters_local, stream);
 }
 
 // ------------------------------------------------------------------------------------------

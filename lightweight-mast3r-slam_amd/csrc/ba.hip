@@ -842,7 +842,7 @@ __device__ __forceinline__ void sp_factor_column_at(const BaArgs& a, const SpTab
       v2[c] = fma(-l2, lc, v2[c]);
     }
   }
-  if (fail && lane == 0) *bad = 1;
+  if (fail && lane == 0) atomicOr(bad, BA_BAD_LLT);
   if (lane < 7) {  // 1/L_mm in column 7 of the diagonal block (used by the back substitution)
     double iv = inv[0];
 #pragma unroll
@@ -945,21 +945,24 @@ __device__ __forceinline__ void flow_st(int* p, int v) {
 }
 
 // wait until every source column of group range gr is factored and `cnt` (when non-null) reads q; wave-uniform
-// Spins are bounded (~2^20 polls, tens of ms): a schedule that could not complete marks the factorisation failed
-// (dx = 0) instead of hanging the workgroup.
+// Spins are bounded (~2^20 polls, tens of ms): a schedule that could not complete sets the STALL bit of `bad`
+// (BA_BAD_STALL: dx = 0, the GN loop ends, and the host returns M3S_ESTALL) instead of hanging the workgroup. A
+// wait abandoned because another wave already failed (a non-positive pivot, BA_BAD_LLT) is not a stall.
+// force_stall (M3S_BA_FORCE_STALL, tests only): the wait is never satisfied.
 constexpr int FLOW_MAX_SPINS = 1 << 20;
 __device__ __forceinline__ void flow_wait_task(const SpTables& T, int2 gr, const int* fac, const int* cnt, int q,
-                                               int lane, int* bad) {
+                                               int lane, int* bad, bool force_stall) {
   const int ns = gr.y - gr.x;
   for (int base = 0; base == 0 || base < ns; base += 63) {
     const bool cs = lane < 63 && base + lane < ns;
     const int k = cs ? T.src[gr.x + base + lane].y : 0;
     const bool cc = lane == 63 && base == 0 && cnt != nullptr;
     int spins = 0;
-    while (__ballot((cs && flow_ld(&fac[k]) == 0) || (cc && flow_ld(cnt) != q)) != 0) {
+    while (__ballot((cs && flow_ld(&fac[k]) == 0) || (cc && flow_ld(cnt) != q) || force_stall) != 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > FLOW_MAX_SPINS || *(volatile int*)bad) {  // stalled, or already failed: stop waiting
-        if (lane == 0) *bad = 1;
+      if (*(volatile int*)bad) return;  // already failed (or stalled) elsewhere: stop waiting
+      if (++spins > FLOW_MAX_SPINS) {
+        if (lane == 0) atomicOr(bad, BA_BAD_STALL);
         return;
       }
     }
@@ -998,8 +1001,9 @@ __device__ __forceinline__ void sp_back_column_flow(const BaArgs& a, const SpTab
     int spins = 0;
     while (__ballot(c && flow_ld(&xd[i]) == 0) != 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > FLOW_MAX_SPINS || *(volatile int*)bad) {
-        if (lane == 0) *bad = 1;
+      if (*(volatile int*)bad) break;
+      if (++spins > FLOW_MAX_SPINS) {
+        if (lane == 0) atomicOr(bad, BA_BAD_STALL);
         break;
       }
     }
@@ -1126,14 +1130,14 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
         const int j = tk.x, gp = T.pull_grp[j];
         const int4 gq = gp >= 0 ? T.grp[gp] : make_int4(0, 0, 0, 0);
         const int2 gr = make_int2(gq.y, gq.z);
-        flow_wait_task(T, gr, f_fac, &f_app[j], tk.y, lane, &s_bad);
+        flow_wait_task(T, gr, f_fac, &f_app[j], tk.y, lane, &s_bad, a.force_stall);
         TST(2 * t);
         sp_factor_column_at(a, T, j, T.col_ptr[j], T.col_ptr[j + 1], gp >= 0, gr, lane, s_red[w], &s_bad);
         if (lane == 0) flow_st(&f_fac[j], 1);
       } else {
         const int4 gq = T.grp[-1 - tk.x];
         const int2 gr = make_int2(gq.y, gq.z);
-        flow_wait_task(T, gr, f_fac, &f_app[gq.x], tk.y, lane, &s_bad);
+        flow_wait_task(T, gr, f_fac, &f_app[gq.x], tk.y, lane, &s_bad, a.force_stall);
         TST(2 * t);
         sp_update_group_at(a, T, gq.x, T.col_ptr[gq.x], T.col_ptr[gq.x + 1], gr, lane, s_red[w]);
         if (lane == 0) flow_st(&f_app[gq.x], tk.y + 1);
@@ -1177,6 +1181,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   __syncthreads();
   SPST(3 + 2 * nlev);
   const bool failed = s_bad != 0 || (a.wide_steps > 0 && *a.bad != 0);
+  const bool stalled = (s_bad & BA_BAD_STALL) != 0;
   const int n = a.nb * 7;
   float n2 = 0.0f;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -1202,6 +1207,10 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     *a.iters += 1;
     if (sqrtf(sum) < delta_thresh) *a.done = 1;
     *a.info = failed ? 1 : 0;
+    if (stalled) {  // sticky until the next plan; the loop ends (the host reports M3S_ESTALL)
+      *a.stalled = 1;
+      *a.done = 1;
+    }
   }
   SPST(4 + 2 * nlev);
 }

@@ -632,6 +632,10 @@ __global__ void __launch_bounds__(256) dense_finish_kernel(BaArgs a, int K, int 
     const float nrm = sqrtf(s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3]);
     *a.iters += 1;
     if (nrm < delta_thresh) *a.done = 1;
+    if (*a.info == 2) {  // an LDS hand-off stalled (lds_wait_ge): sticky, the loop ends, the host reports M3S_ESTALL
+      *a.stalled = 1;
+      *a.done = 1;
+    }
     *a.info = 0;
   }
 }

@@ -79,4 +79,9 @@ struct BaArgs {
   int* done;   // early-exit flag (|dx| < delta_thresh)
   int* iters;  // iterations executed
   int* bad;    // non-positive pivot seen by a multi-workgroup factor step (cleared by the assembly)
+  int* stalled;  // sticky: a dataflow / LDS hand-off wait timed out in some solve of this plan (M3S_ESTALL)
+  int force_stall;  // tests only (M3S_BA_FORCE_STALL): the dataflow waits are never satisfied
 };
+// bits of the factor kernel's failure word
+#define BA_BAD_LLT 1    // non-positive pivot: dx = 0 for this iteration (SimplicialLLT info != Success)
+#define BA_BAD_STALL 2  // a bounded dataflow wait timed out

@@ -7,6 +7,9 @@ namespace m3s {
 typedef _Float16 h1;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
+// NaN-propagating max (fmaxf drops a NaN operand; the refine screen's norm bound must see one)
+__device__ __forceinline__ float fmaxf_nan(float a, float b) { return (a > b || a != a) ? a : b; }
+
 // D21 row source: f16 (reference signature, caller did .half()) or f32 (fused path: RNE convert here,
 // identical to torch's .half()).
 template <int F, bool D21_F32>

@@ -13,7 +13,8 @@
 #include "m3s_half.hpp"
 
 extern "C" hipError_t m3s_launch_refine_tile(const void*, const void*, const void*, void*, int, int, int, int, int,
-                                             int, int, void*, int*, hipStream_t);
+                                             int, int, void*, int*, const float*, hipStream_t);
+extern "C" int m3s_refine_tile_ok(int, int, int, int, int, int);
 
 namespace m3s {
 
@@ -25,8 +26,9 @@ namespace m3s {
 #define PREP_T 16
 __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict__ X11, float* __restrict__ rays9,
                                                         const float* __restrict__ D11, h1* __restrict__ D11h, int H,
-                                                        int W, int F) {
+                                                        int W, int F, float* __restrict__ cnorm_part, int planar) {
   __shared__ float tile[(PREP_T + 2) * (PREP_T + 2) * 3];
+  __shared__ float s_ss[PREP_T * PREP_T * 8];  // per pixel, per 4-channel group: sum of squares of the f16 values
   const int b = blockIdx.z;
   const int u0 = blockIdx.x * PREP_T, v0 = blockIdx.y * PREP_T;
   const float* Xb = X11 + (size_t)b * H * W * 3;
@@ -73,10 +75,47 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
         const size_t off = (((size_t)b * H + yy) * W + xx) * F + q * 4;
         const float4 v = *reinterpret_cast<const float4*>(D11 + off);
         h1 r[4] = {(h1)v.x, (h1)v.y, (h1)v.z, (h1)v.w};
-        *reinterpret_cast<uint2*>(D11h + off) = *reinterpret_cast<uint2*>(r);
+        // planar (refine tile path, F = 24): image b's chunk plane q / 2 holds (H, W, 8)
+        const size_t hoff = planar ? ((size_t)b * 3 + (q >> 1)) * H * W * 8 + ((size_t)yy * W + xx) * 8 + (q & 1) * 4
+                                   : off;
+        *reinterpret_cast<uint2*>(D11h + hoff) = *reinterpret_cast<uint2*>(r);
+        if (cnorm_part != nullptr) {
+          const float a = (float)r[0], c = (float)r[1], d = (float)r[2], e = (float)r[3];
+          s_ss[pix * 8 + q] = a * a + c * c + d * d + e * e;
+        }
+      } else if (cnorm_part != nullptr) {
+        s_ss[pix * 8 + q] = 0.0f;
       }
     }
+    if (cnorm_part != nullptr) {
+      // the refine screen's descriptor-norm bound (refine.hip): max over this tile's pixels of |D11h[pixel]|_2,
+      // one partial per block; proj_occlusion_kernel reduces the partials before refine reads the maximum.
+      // NaN / inf descriptors give a NaN / inf partial, which switches the screen off for every lane.
+      __syncthreads();
+      float ss = 0.0f;
+      for (int k = 0; k < F / 4; k++) ss += s_ss[threadIdx.x * 8 + k];
+      float nmax = sqrtf(ss);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
+      __syncthreads();  // every s_ss read is done: reuse the first words for the wave maxima
+      if ((threadIdx.x & 63) == 0) s_ss[threadIdx.x >> 6] = nmax;
+      __syncthreads();
+      if (threadIdx.x == 0)
+        cnorm_part[((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
+            fmaxf_nan(fmaxf_nan(s_ss[0], s_ss[1]), fmaxf_nan(s_ss[2], s_ss[3]));
+    }
   }
+}
+
+// max of the prep partials into cmax[0] (the screen's descriptor-norm bound), by the first wave of block 0 of
+// the launch that runs between prep and refine
+__device__ __forceinline__ void reduce_cnorm(const float* __restrict__ part, int nparts, float* __restrict__ cmax) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.0f;
+  for (int i = lane; i < nparts; i += 64) m = fmaxf_nan(m, part[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf_nan(m, __shfl_xor(m, off, 64));
+  if (lane == 0) *cmax = m;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -194,8 +233,10 @@ __global__ void __launch_bounds__(256) iter_proj_kernel(const float* __restrict_
 __global__ void __launch_bounds__(256) proj_occlusion_kernel(
     const float* __restrict__ rays, const float* __restrict__ X11, const float* __restrict__ X21,
     const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
-    int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter) {
+    int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter,
+    const float* __restrict__ cnorm_part, int cnorm_nparts, float* __restrict__ cmax) {
   const int N = H * W;
+  if (cmax != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) reduce_cnorm(cnorm_part, cnorm_nparts, cmax);
   // contiguous pixel runs per XCD: each XCD's L2 then holds the rays rows its LM gathers touch
   const int n = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
@@ -353,11 +394,18 @@ __global__ void __launch_bounds__(256) refine_f32_kernel(const float* __restrict
 // ------------------------------------------------------------------------------------------
 // launchers (called from abi.cpp)
 // ------------------------------------------------------------------------------------------
+// cnorm_part (nullable): m3s_prep_parts(B, H, W) floats, the per-block descriptor-norm maxima (F <= 32)
+extern "C" int m3s_prep_parts(int B, int H, int W) {
+  return ((W + PREP_T - 1) / PREP_T) * ((H + PREP_T - 1) / PREP_T) * B;
+}
+
 extern "C" hipError_t m3s_launch_prep(const float* X11, float* rays9, const float* D11, void* D11h, int B, int H,
-                                      int W, int F, hipStream_t s) {
+                                      int W, int F, float* cnorm_part, int planar, hipStream_t s) {
+  if (planar && F != 24) return hipErrorInvalidValue;
+  if (F > 32 || F % 4 != 0) cnorm_part = nullptr;
   dim3 grid((W + PREP_T - 1) / PREP_T, (H + PREP_T - 1) / PREP_T, B);
   hipLaunchKernelGGL(m3s::prep_rays_kernel, grid, dim3(256), 0, s, X11, rays9, D11,
-                     reinterpret_cast<m3s::h1*>(D11h), H, W, F);
+                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, D11 != nullptr ? cnorm_part : nullptr, planar);
   return hipGetLastError();
 }
 
@@ -373,10 +421,11 @@ extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, 
 extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* X11, const float* X21,
                                                 const int64_t* idx_init, int* p1, uint8_t* valid, int B, int H, int W,
                                                 int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-                                                int* zero_counter, hipStream_t s) {
+                                                int* zero_counter, const float* cnorm_part, int cnorm_nparts,
+                                                float* cmax, hipStream_t s) {
   dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
-                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter);
+                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter, cnorm_part, cnorm_nparts, cmax);
   return hipGetLastError();
 }
 
@@ -386,7 +435,7 @@ extern "C" hipError_t m3s_launch_refine_f16(const void* D11, const void* D21, co
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11);
   const m3s::h1* q = reinterpret_cast<const m3s::h1*>(D21);
   if (N == H * W &&
-      m3s_launch_refine_tile(D11, D21, p1, p1_new, B, H, W, F, radius, dilation_max, 0, nullptr, nullptr, s) ==
+      m3s_launch_refine_tile(D11, D21, p1, p1_new, B, H, W, F, radius, dilation_max, 0, nullptr, nullptr, nullptr, s) ==
           hipSuccess)
     return hipSuccess;  // tiled LDS path (query n is pixel n of the grid)
   switch (F) {
@@ -420,13 +469,12 @@ extern "C" hipError_t m3s_launch_refine_f32(const float* D11, const float* D21, 
 // olist/ocount: deferred-outlier list (B*H*W int4) + counter, zeroed by proj_occlusion_kernel
 extern "C" hipError_t m3s_launch_refine_lin(const void* D11h, const float* D21, const int* p1, int64_t* idx_out, int B,
                                             int H, int W, int F, int radius, int dilation_max, void* olist,
-                                            int* ocount, hipStream_t s) {
+                                            int* ocount, const float* cmax, hipStream_t s) {
   dim3 grid((H * W + 255) / 256, B);
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
-  if (radius > 0 &&
-      m3s_launch_refine_tile(D11h, D21, p1, idx_out, B, H, W, F, radius, dilation_max, 1, olist, ocount, s) ==
-          hipSuccess)
-    return hipSuccess;  // tiled LDS path
+  // tiled LDS path exactly when m3s_refine_tile_ok (prep wrote the PLANAR D11h then)
+  if (radius > 0 && m3s_refine_tile_ok(B, H, W, F, radius, dilation_max))
+    return m3s_launch_refine_tile(D11h, D21, p1, idx_out, B, H, W, F, radius, dilation_max, 1, olist, ocount, cmax, s);
   switch (F) {
     case 24:
       hipLaunchKernelGGL(m3s::refine_lin_kernel<24>, grid, dim3(256), 0, s, a, D21, p1, idx_out, H, W, radius,

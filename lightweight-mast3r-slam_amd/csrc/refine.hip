@@ -51,16 +51,30 @@ __device__ unsigned long long g_refine_bstamps[8192 * 4];
 // One level of one pixel by the whole wave (cu, cv, max_score, sq wave-uniform): lane c < 49 scores
 // candidate (c / 7, c % 7) from global memory; the first candidate in scan order holding the wave
 // maximum wins if it beats the running max — the sequential strict-'>' scan's result.
-template <int D>
+// D11h layouts: PLANAR (fused path, written by prep_rays_kernel) = per image three chunk planes (H,W,8) f16, so a
+// window row of one chunk is one contiguous 16 B-per-pixel run; otherwise the caller's (H,W,24) f16.
+template <bool PLANAR>
+__device__ __forceinline__ const h1* pix_ptr(const h1* img, size_t pix) {
+  return img + pix * (PLANAR ? 8 : 24);
+}
+template <bool PLANAR>
+__device__ __forceinline__ void load_chunks(const h1* p, size_t N, uint4& c0, uint4& c1, uint4& c2) {
+  const size_t cs = PLANAR ? N * 8 : 8;  // chunk stride in halves
+  c0 = *reinterpret_cast<const uint4*>(p);
+  c1 = *reinterpret_cast<const uint4*>(p + cs);
+  c2 = *reinterpret_cast<const uint4*>(p + 2 * cs);
+}
+
+template <int D, bool PLANAR>
 __device__ __forceinline__ void wave_level(const h1* __restrict__ img, int H, int W, const h2* sq, int& cu, int& cv,
                                            h1& max_score, int lane) {
-  constexpr int R = 3, RD = R * D, F = 24, G = 2 * R + 1;
+  constexpr int R = 3, RD = R * D, G = 2 * R + 1;
   const int ci = lane / G, cj = lane % G;
   const int u = cu - RD + ci * D, v = cv - RD + cj * D;
   const bool ok = lane < G * G && u >= 0 && u < W && v >= 0 && v < H;
-  const uint4* p =
-      reinterpret_cast<const uint4*>(img + ((size_t)min(max(v, 0), H - 1) * W + min(max(u, 0), W - 1)) * F);
-  const uint4 c0 = p[0], c1 = p[1], c2 = p[2];
+  uint4 c0, c1, c2;
+  load_chunks<PLANAR>(pix_ptr<PLANAR>(img, (size_t)min(max(v, 0), H - 1) * W + min(max(u, 0), W - 1)),
+                      (size_t)H * W, c0, c1, c2);
   h1 sc = (h1)0.0f;
   add8(sc, &sq[0], c0);
   add8(sc, &sq[4], c1);
@@ -90,6 +104,68 @@ __device__ __forceinline__ void score_chunk(const uint4* base, const h2* q4, h1*
   }
 }
 
+// Bound-screened refine (SCREEN): the level's 49 candidates are first scored by an fp32 dot of the same half operands
+// (v_dot2c_f32_f16: 12 per candidate instead of 24 half products + 24 half adds), then only candidates whose screen
+// score lies within the rounding bound of the level's best are scored by the exact c10::Half chain, in scan order.
+// The result is the sequential scan's, bit for bit:
+//   * |S_half - S_real| <= 24 u P + 24 * 2^-25 for the c10::Half chain (u = 2^-11: 24 product roundings, 23 add
+//     roundings, each <= u times a partial sum <= (1 + 0.013) P), where P = sum |q_k c_k| <= |q|_2 |c|_2, and
+//     |S_dot2 - S_real| <= 12 (3 * 2^-24 P + 2^-36) (measured on gfx950, scripts/micro/dot2_exact.hip: at most
+//     3 fp32 roundings of |a0 b0| + |a1 b1| + |acc| per instruction, 2^-36 absolute with subnormal halves);
+//     so B = 0.0125 |q| cmax + 2^-18 bounds |S_half - S_dot2| (24 u = 0.01172), cmax = max |D11h[pixel]|_2
+//     over the image (prep_rays_kernel).
+//   * The winner w (first candidate in scan order with S_half[w] = M = max S_half, when M beats the running max)
+//     has S_dot2[w] >= M - B >= Lmax - 2B, where Lmax = max over in-image candidates of S_dot2 (M >= S_half[c] >=
+//     S_dot2[c] - B), and S_dot2[w] > max_score - B. A candidate failing either cannot win nor tie the winner,
+//     so the scan over the survivors alone (ascending order, strict '>') returns the full scan's result.
+//   * After the first level the centre candidate (3,3) is the last winner (its score IS the running max) or the
+//     start pixel that did not beat +0: it never wins a strict '>' and is dropped from the survivors.
+//   * |q| cmax > 16384 (overflow range) or non-finite: every in-image candidate survives (exact for all).
+template <int D>
+__device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, float* a) {
+  constexpr int G = 7;
+#pragma unroll
+  for (int i = 0; i < G; i++) {
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      const uint4 c = base[j * D * RT_COLS + i * D];
+      const h2* cv = reinterpret_cast<const h2*>(&c);
+      float t = a[i * G + j];
+#pragma unroll
+      for (int k = 0; k < 4; k++) t = __builtin_amdgcn_fdot2(q4[k], cv[k], t, false);
+      // pin the column's dot products here: otherwise the last chunk's are sunk into the survivor code and
+      // all 49 candidate loads stay live across it (1000+ spilled VGPRs)
+      asm volatile("" : "+v"(t));
+      a[i * G + j] = t;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// exact c10::Half chains of the survivor mask m in ascending scan order, read from D11h (L2); strict '>'
+template <int D, bool PLANAR>
+__device__ __forceinline__ void exact_survivors(const h1* __restrict__ img, int H, int W, const h2* q, int u_lo,
+                                                int v_lo, uint64_t m, h1& max_score, int& bi) {
+  while (__ballot(m != 0)) {  // wave-uniform trip count: the lane with the most survivors
+    if (m != 0) {
+      const int c = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int i = c / 7, j = c - 7 * i;
+      uint4 c0, c1, c2;
+      load_chunks<PLANAR>(pix_ptr<PLANAR>(img, (size_t)(v_lo + j * D) * W + (u_lo + i * D)), (size_t)H * W, c0, c1,
+                          c2);
+      h1 sc = (h1)0.0f;
+      add8(sc, &q[0], c0);
+      add8(sc, &q[4], c1);
+      add8(sc, &q[8], c2);
+      if (sc > max_score) {
+        max_score = sc;
+        bi = c;
+      }
+    }
+  }
+}
+
 struct TileCtx {
   const h1* img;
   int H, W, lane, wid, u_pix, v_pix;
@@ -97,11 +173,13 @@ struct TileCtx {
   int bn;       // batch * N + pixel
   int4* olist;  // deferred-pixel list (nullable: score outliers in place)
   int* ocount;
+  float bq;      // SCREEN: this lane's bound B (0.0125 |q| cmax + 2^-18)
+  bool sok;      // SCREEN: the bound is usable (|q| cmax <= 16384 and finite)
 };
 
-template <int D>
+template <int D, bool SCREEN, bool PLANAR>
 __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, const h2* q, int& cu, int& cv,
-                                             h1& max_score, uint4* lds, int (*s_red)[4]) {
+                                             h1& max_score, uint4* lds, int (*s_red)[4], bool first) {
   constexpr int R = 3, G = 2 * R + 1, F = 24, RD = R * D;
   const int lane = t.lane, wid = t.wid, H = t.H, W = t.W;
   // bbox of the inlier centres (within 16 px of pixel + the tile's flow estimate t.fu/t.fv)
@@ -177,7 +255,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
           const int v = __shfl(*reinterpret_cast<const int*>(&q[k]), src, 64);
           sq[k] = *reinterpret_cast<const h2*>(&v);
         }
-        wave_level<D>(t.img, H, W, sq, scu, scv, smax, lane);
+        wave_level<D, PLANAR>(t.img, H, W, sq, scu, scv, smax, lane);
         if (lane == src) {
           cu = scu;
           cv = scv;
@@ -186,18 +264,66 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       }
     }
   }
+  // per-lane column offset; the row base (and the chunk plane) is wave-uniform (scalar)
+  const int lane_off = gx * (PLANAR ? 8 : F);
+  const size_t cstride = PLANAR ? (size_t)H * W * 8 : 8, rstride = (size_t)W * (PLANAR ? 8 : F);
+  if constexpr (SCREEN) {
+    float a[G * G];
+#pragma unroll
+    for (int c = 0; c < G * G; c++) a[c] = 0.0f;
+    __syncthreads();  // the reduction scratch aliases the window: its readers are done
+#pragma unroll
+    for (int chunk = 0; chunk < F / 8; chunk++) {
+      if (chunk) __syncthreads();
+      for (int y = wid; y < nrows; y += 4) {
+        const int gy = min(max(wy0 + y, 0), H - 1);
+        const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
+        __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (lane_in) screen_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], a);
+    }
+    if (lane_in) {
+      uint64_t vm = (1ull << (G * G)) - 1ull;  // in-image candidates
+      if (__ballot(lane_in && !(u_lo >= 0 && u_lo + 6 * D < W && v_lo >= 0 && v_lo + 6 * D < H)) != 0) {
+        uint64_t jm = 0;
+#pragma unroll
+        for (int j = 0; j < G; j++) jm |= (v_lo + j * D >= 0 && v_lo + j * D < H) ? (1ull << j) : 0ull;
+        vm = 0;
+#pragma unroll
+        for (int i = 0; i < G; i++) vm |= (u_lo + i * D >= 0 && u_lo + i * D < W) ? (jm << (i * G)) : 0ull;
+      }
+      float lmax = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < G * G; c++) lmax = fmaxf(lmax, ((vm >> c) & 1ull) ? a[c] : -INFINITY);
+      const float T = fmaxf((float)max_score - t.bq, lmax - 2.0f * t.bq);
+      uint64_t m = 0;
+#pragma unroll
+      for (int c = 0; c < G * G; c++) m |= (a[c] >= T) ? (1ull << c) : 0ull;
+      if (!t.sok) m = ~0ull;
+      m &= vm;
+      if (!first) m &= ~(1ull << (G * G / 2));
+      int bi = -1;
+      exact_survivors<D, PLANAR>(t.img, H, W, q, u_lo, v_lo, m, max_score, bi);
+      if (bi >= 0) {
+        cu = u_lo + (bi / G) * D;
+        cv = v_lo + (bi % G) * D;
+      }
+    }
+    return;
+  }
   h1 s[G * G];
 #pragma unroll
   for (int c = 0; c < G * G; c++) s[c] = (h1)0.0f;
   __syncthreads();  // the reduction scratch aliases the window: its readers are done
-  const int lane_off = gx * F;  // per-lane column offset; the row base is wave-uniform (scalar)
 #pragma unroll
   for (int chunk = 0; chunk < F / 8; chunk++) {
     if (chunk) __syncthreads();  // previous chunk's readers are done
 #ifndef RT_NOLOAD
     for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
-      const h1* rowp = t.img + (size_t)gy * W * F + chunk * 8;
+      const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
       __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
     }
 #endif
@@ -259,12 +385,14 @@ __device__ __forceinline__ void store_out(void* outv, size_t bn, int W, int cu, 
 }
 
 // P1_I64: p1 given as (B,N,2) int64 (reference op) else int32 (fused); LIN_OUT: write idx = u + W v.
-template <bool D21_F32, bool P1_I64, bool LIN_OUT>
+// SCREEN: bound-screened scoring (cmaxp = the descriptor-norm bound written by prep / proj_occlusion).
+// LIN_OUT (fused path) reads the PLANAR D11h of prep_rays_kernel.
+template <bool D21_F32, bool P1_I64, bool LIN_OUT, bool SCREEN>
 __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
                                                              const void* __restrict__ p1v, void* __restrict__ outv,
                                                              int H, int W, int dilation_max, int tiles_x,
                                                              int tiles_per_img, int nblocks, int4* olist,
-                                                             int* ocount) {
+                                                             int* ocount, const float* __restrict__ cmaxp) {
   constexpr int F = 24;
   __shared__ uint4 lds[RT_ROWS * RT_COLS];
   int(*s_red)[4] = reinterpret_cast<int(*)[4]>(&lds[0]);  // level-start reductions alias the window
@@ -313,21 +441,32 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
     t.fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
     t.fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
   }
+  t.bq = 0.0f;
+  t.sok = false;
+  if constexpr (SCREEN) {
+    float qq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < F / 2; k++) qq = __builtin_amdgcn_fdot2(q[k], q[k], qq, false);
+    const float pq = sqrtf(qq) * *cmaxp * 1.001f;  // |q|_2 |c|_2 bound, rounded up
+    t.sok = pq <= 16384.0f;                         // false for NaN / inf
+    t.bq = t.sok ? 0.0125f * pq + 0x1p-18f : 0.0f;
+  }
   const bool mine = active;  // deferred pixels are written by refine_outlier_kernel
 #ifdef M3S_REFINE_BSTAMPS
   if (threadIdx.x == 0 && blockIdx.x < 8192) g_refine_bstamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
   h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
   for (int d = dilation_max; d > 0; d--) {
+    const bool first = d == dilation_max;
     switch (d) {
-      case 8: refine_level<8>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 7: refine_level<7>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 6: refine_level<6>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 5: refine_level<5>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 4: refine_level<4>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 3: refine_level<3>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      case 2: refine_level<2>(t, active, q, cu, cv, max_score, lds, s_red); break;
-      default: refine_level<1>(t, active, q, cu, cv, max_score, lds, s_red); break;
+      case 8: refine_level<8, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 7: refine_level<7, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 6: refine_level<6, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 5: refine_level<5, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 4: refine_level<4, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 3: refine_level<3, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 2: refine_level<2, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      default: refine_level<1, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
     }
   }
   if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
@@ -373,14 +512,14 @@ __global__ void __launch_bounds__(256) refine_outlier_kernel(const h1* __restric
     load_query<F, D21_F32>(D21, bn, q);
     for (int d = d0; d > 0; d--) {
       switch (d) {
-        case 8: wave_level<8>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 7: wave_level<7>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 6: wave_level<6>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 5: wave_level<5>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 4: wave_level<4>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 3: wave_level<3>(img, H, W, q, cu, cv, max_score, lane); break;
-        case 2: wave_level<2>(img, H, W, q, cu, cv, max_score, lane); break;
-        default: wave_level<1>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 8: wave_level<8, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 7: wave_level<7, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 6: wave_level<6, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 5: wave_level<5, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 4: wave_level<4, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 3: wave_level<3, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 2: wave_level<2, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        default: wave_level<1, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
       }
     }
     if (lane == 0) store_out<LIN_OUT>(outv, bn, W, cu, cv);
@@ -389,25 +528,35 @@ __global__ void __launch_bounds__(256) refine_outlier_kernel(const h1* __restric
 
 }  // namespace m3s
 
+// shapes the tile kernel takes (else the per-pixel kernels of matching.hip); the fused path's prep writes the
+// PLANAR D11h exactly when this holds
+extern "C" int m3s_refine_tile_ok(int B, int H, int W, int F, int radius, int dilation_max) {
+  if (F != 24 || radius != 3 || dilation_max < 1 || dilation_max > 8) return 0;
+  if ((long long)B * H * W >= (1ll << 31) || H >= 32768 || W >= 32768) return 0;
+  return 1;
+}
+
 // D21 f32 + p1 int32 -> idx (fused path) or D21 f16 + p1 int64 -> p1_new (reference op).
 // olist/ocount (nullable): deferred-outlier list of >= B*H*W int4 and its counter, zeroed on the
 // stream before this launch. Returns hipErrorNotSupported when the shape is not eligible (the
 // caller falls back to the per-pixel kernels).
 extern "C" hipError_t m3s_launch_refine_tile(const void* D11h, const void* D21, const void* p1, void* out, int B,
                                              int H, int W, int F, int radius, int dilation_max, int fused,
-                                             void* olist, int* ocount, hipStream_t s) {
-  if (F != 24 || radius != 3 || dilation_max < 1 || dilation_max > 8) return hipErrorNotSupported;
-  if ((long long)B * H * W >= (1ll << 31) || H >= 32768 || W >= 32768) return hipErrorNotSupported;
+                                             void* olist, int* ocount, const float* cmax, hipStream_t s) {
+  if (!m3s_refine_tile_ok(B, H, W, F, radius, dilation_max)) return hipErrorNotSupported;
   const int tx = (W + RT_TW - 1) / RT_TW, ty = (H + RT_TH - 1) / RT_TH, nb = tx * ty * B;
   const m3s::h1* a = reinterpret_cast<const m3s::h1*>(D11h);
   int4* ol = reinterpret_cast<int4*>(olist);
   if (ol == nullptr) ocount = nullptr;
-  if (fused)
-    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true>), dim3(nb), dim3(256), 0, s, a, D21, p1, out, H, W,
-                       dilation_max, tx, tx * ty, nb, ol, ocount);
+  if (fused && cmax != nullptr)
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, true>), dim3(nb), dim3(256), 0, s, a, D21, p1, out,
+                       H, W, dilation_max, tx, tx * ty, nb, ol, ocount, cmax);
+  else if (fused)
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, false>), dim3(nb), dim3(256), 0, s, a, D21, p1, out,
+                       H, W, dilation_max, tx, tx * ty, nb, ol, ocount, nullptr);
   else
-    hipLaunchKernelGGL((m3s::refine_tile_kernel<false, true, false>), dim3(nb), dim3(256), 0, s, a, D21, p1, out, H,
-                       W, dilation_max, tx, tx * ty, nb, ol, ocount);
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<false, true, false, false>), dim3(nb), dim3(256), 0, s, a, D21, p1,
+                       out, H, W, dilation_max, tx, tx * ty, nb, ol, ocount, nullptr);
   if (ol != nullptr) {
     const int ob = 1024;  // 4096 waves: one pass over a few thousand deferred pixels, idle waves exit
     if (fused)

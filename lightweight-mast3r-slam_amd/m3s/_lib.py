@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # M3S_LIB: alternative build of the same library (kernel experiments); still the HIP library, no fallback
 LIB_PATH = os.environ.get("M3S_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libm3s.so")
 
-ABI_VERSION = 4  # include/m3s.h M3S_ABI_VERSION
+ABI_VERSION = 5  # include/m3s.h M3S_ABI_VERSION
 
 c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
 

@@ -185,4 +185,5 @@ def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter
     if info is not None:
         info["packed_edges"], info["changed_keyframes"] = shard.reuse_info()
     run_sharded(shard, max_iter, group)
+    shard.iterations()  # one readback: raises RuntimeError (M3S_ESTALL) if a factor-schedule wait timed out
     return [shard.dx]

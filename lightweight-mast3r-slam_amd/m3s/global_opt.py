@@ -125,6 +125,16 @@ class FactorGraph:
         T_WCs = Sim3(torch.stack([kf.T_WC.data.reshape(1, 8) for kf in kfs]))
         return T_WCs, (X, C, [float(kf.N) for kf in kfs])
 
+    @staticmethod
+    def _pin(cfg):
+        """cfg.pin: the C++ solvers fix exactly one pose (num_fix = 1, gn_kernels.cu:741,1157,1566) while the
+        Python slices the write-back by cfg.pin (global_opt.py:125,161), so any other pin would write poses the
+        solve held fixed (or drop solved ones): rejected (SURVEY.md §8 a-note 8)."""
+        pin = cfg["pin"]
+        if pin != 1:
+            raise ValueError(f"local_opt.pin = {pin}: only pin = 1 is supported (the solver fixes one pose)")
+        return pin
+
     def _sharded(self):
         return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
 
@@ -145,7 +155,7 @@ class FactorGraph:
     def solve_GN_rays(self):
         """global_opt.py:123-161, with the keyframe points read in place (no torch.stack of K x N x 16 B)."""
         cfg = self.cfg
-        pin = cfg["pin"]
+        pin = self._pin(cfg)
         unique_kf_idx = self.get_unique_kf_idx()
         if unique_kf_idx.numel() <= pin:
             return
@@ -178,7 +188,7 @@ class FactorGraph:
         """global_opt.py:163-226."""
         cfg = self.cfg
         K = self.K
-        pin = cfg["pin"]
+        pin = self._pin(cfg)
         unique_kf_idx = self.get_unique_kf_idx()
         if unique_kf_idx.numel() <= pin:
             return

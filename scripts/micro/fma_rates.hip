@@ -72,6 +72,10 @@ KERNEL(k_pk_fma_f32, double, "v_pk_fma_f32 %0, %0, %1, %1")
 KERNEL(k_pk_mul_f32, double, "v_pk_mul_f32 %0, %0, %1")
 KERNEL(k_fma_f64, double, "v_fma_f64 %0, %0, %1, %1")
 KERNEL(k_add_f64, double, "v_add_f64 %0, %0, %1")
+// refine screening (bit-exact screened refine): fp32 dot of two half pairs, VOP2 accumulate and VOP3P forms
+KERNEL(k_dot2c_f32_f16, float, "v_dot2c_f32_f16 %0, %1, %1")
+KERNEL(k_dot2_f32_f16, float, "v_dot2_f32_f16 %0, %1, %1, %0")
+KERNEL(k_max3_f32, float, "v_max3_f32 %0, %0, %1, %1")
 
 typedef void (*kfn)(void*, unsigned long long*, int);
 
@@ -101,6 +105,8 @@ int main() {
       {"v_fma_f16_hi1", (const void*)k_fma_f16_hi1, 4}, {"v_mad_f16_hi1", (const void*)k_mad_f16_hi1, 4},
       {"v_fma_f16_v3", (const void*)k_fma_f16_v3, 4}, {"v_pk_add_f16_sel", (const void*)k_pk_add_f16_sel, 4},
       {"v_fma_f64", (const void*)k_fma_f64, 8},       {"v_add_f64", (const void*)k_add_f64, 8},
+      {"v_dot2c_f32_f16", (const void*)k_dot2c_f32_f16, 4}, {"v_dot2_f32_f16", (const void*)k_dot2_f32_f16, 4},
+      {"v_max3_f32", (const void*)k_max3_f32, 4},
   };
   const int iters = 4000;
   printf("gfx950 VALU issue cost per wave64 instruction per SIMD (median over %d CUs, one block per CU):\n"

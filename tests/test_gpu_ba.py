@@ -340,3 +340,42 @@ def test_rccl_all_reduce_path_equals_unsharded(tmp_path):
     print(r.stdout[-3000:], r.stderr[-3000:])
     assert r.returncode == 0, r.stderr[-3000:]
     assert "RCCL_BA_OK" in r.stdout
+
+
+def test_factor_schedule_stall_raises_not_silent(monkeypatch):
+    """A dataflow hand-off wait of the device factorisation that times out (a schedule fault) is an error
+    (M3S_ESTALL -> RuntimeError), never the silent dx = 0 of a non-positive pivot (gn_kernels.cu:142-150, which
+    test_singular_system_returns_zero_step keeps). M3S_BA_FORCE_STALL makes every dataflow wait unsatisfiable;
+    the bounded spin (~2^20 polls) then gives up. The next plan without it solves normally."""
+    from m3s.config import config
+    from m3s.dist_ba import HipShard, ba_config, gauss_newton_sharded
+    from m3s.synthetic import make_graph, two_way
+
+    monkeypatch.setenv("M3S_BA_SOLVER", "sparse")
+    G = make_graph(n_kf=48, H=12, W=16, seed=3)
+    ii, jj, idx, valid, Q = two_way(G)
+    dev = torch.device("cuda")
+    cfg = ba_config("rays", config["local_opt"])
+    args = lambda T: (cfg, T, G["Xs"].to(dev).contiguous(), G["Cs"][..., 0].to(dev).contiguous(), ii.to(dev),
+                      jj.to(dev), idx.to(dev).contiguous(), valid[..., 0].to(dev).contiguous(),
+                      Q[..., 0].to(dev).contiguous(), 0.0, 0, ii.shape[0])
+    monkeypatch.setenv("M3S_BA_FORCE_STALL", "1")
+    T0 = G["Twc0"].to(dev).contiguous()
+    sh = HipShard(*args(T0))
+    sh.linearize()
+    sh.solve()
+    with pytest.raises(RuntimeError, match="stall"):
+        sh.iterations()
+    assert torch.equal(T0, G["Twc0"].to(dev))  # the stalled iteration did not move the poses
+    # the full call surfaces it too
+    with pytest.raises(RuntimeError, match="stall"):
+        gauss_newton_sharded("rays", G["Twc0"].to(dev).contiguous(), G["Xs"].to(dev).contiguous(),
+                             G["Cs"][..., 0].to(dev).contiguous(), ii.to(dev), jj.to(dev), idx.to(dev).contiguous(),
+                             valid[..., 0].to(dev).contiguous(), Q[..., 0].to(dev).contiguous(), config["local_opt"],
+                             2, 1e-8)
+    monkeypatch.delenv("M3S_BA_FORCE_STALL")
+    T1 = G["Twc0"].to(dev).contiguous()
+    sh = HipShard(*args(T1))
+    sh.linearize()
+    sh.solve()
+    assert sh.iterations() == 1 and not torch.equal(T1, G["Twc0"].to(dev))
