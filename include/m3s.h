@@ -148,7 +148,7 @@ int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /*
 /* Host-only facts of a built plan (bench rooflines, tests): info[0] = linearisation chunks per edge,
  * [1] = factor blocks, [2] = elimination-tree levels, [3] = multi-workgroup factor steps, [4] = 1 if the dense
  * fallback factorisation is used, [5] = distinct target keyframes among the shard's edges, [6] = shard edges,
- * [7] = poses. */
+ * [7] = poses, [8] = factor steps run by the subtree phase (one launch), [9] = its workgroups. info holds 10 ints. */
 int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info);
 /* Host-only diagnostic of the symbolic factorisation the plan builds for these edges (host arrays):
  * stats[0] = factor blocks (7x7, diagonal included), [1] = elimination-tree levels, [2] = update groups
@@ -225,6 +225,15 @@ typedef struct m3s_track_fuse_args {
   float* Ck_avg_out;     /* (N)   fused C / Nk_new = keyframe.get_average_conf() (nullable) */
   float* Cf_avg_out;     /* (N)   Cf / Nf = frame.get_average_conf() (nullable) */
   float Nk_new, Nf;      /* keyframe N after this fusion, frame N (frame.py:83-84) */
+  /* keyframe-store slot write-back (nullable; SharedKeyframes.__setitem__, frame.py:271-289, called at
+   * tracker.py:101): with Xk_out / Ck_out pointing INTO the store's X[idx] / C[idx] rows, the fusion kernel also
+   * stores the slot's fusion counters and dirty flag, on the device, when the frame tracked (the fusion's own
+   * condition): slot_N = N_new, slot_N_updates = N_updates_new, slot_dirty = 1. Nothing else of the record changes
+   * on a track (img, uimg, feat, pos, T_WC keep their values), so no full-record copy is needed. */
+  int* slot_N;
+  int* slot_N_updates;
+  uint8_t* slot_dirty;
+  int N_new, N_updates_new;
 } m3s_track_fuse_args;
 
 typedef struct m3s_track_result {

@@ -429,6 +429,11 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     fa.Cf_avg = fuse->Cf_avg_out;
     fa.Nk_new = fuse->Nk_new;
     fa.Nf = fuse->Nf;
+    fa.slot_N = fuse->slot_N;
+    fa.slot_N_updates = fuse->slot_N_updates;
+    fa.slot_dirty = fuse->slot_dirty;
+    fa.N_new = fuse->N_new;
+    fa.N_updates_new = fuse->N_updates_new;
   }
   // the previous frame's fuse launch left this workspace's scratch clean (byte map of n16 entries, counters,
   // tickets): track_init runs only for a fresh / grown / failed workspace
@@ -532,7 +537,9 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_SYM_SECTIONS = 16;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_SYM_SECTIONS = 17;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
+constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
 constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
@@ -548,6 +555,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       (size_t)E * chunks +  // + the linearisation block table
                       2 * (size_t)E +       // + record slots and the pack list (record reuse)
                       8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + wide-step task records
+                      8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + subtree task records
+                      4 * (size_t)BA_SUB_MAX_WG * BA_MAX_WIDE_STEPS +                      //   and their step table
                       2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm);  // + the dataflow schedule
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
@@ -689,6 +698,7 @@ struct PlanSym {
   std::vector<char> image;  // the tables, packed at 16-B aligned offsets, as uploaded
   size_t off[BA_SYM_SECTIONS] = {0};
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
+  int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
   int step_na[BA_MAX_WIDE_STEPS] = {0};    // its factor tasks (update groups follow)
@@ -733,10 +743,11 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     if (!strcmp(f, "sparse")) Y->dense = 0;
     if (!strcmp(f, "dense") && has_dense) Y->dense = 1;
   }
-  // the leaf end of the elimination tree runs as multi-workgroup launches (steps [0, wide_steps)), the root end
-  // in the one-workgroup kernel. The split minimises the measured step costs (MI355X, C5/C4 graphs): a launch
-  // ~5.8 us per step, a step inside the workgroup ~3.7 us per round of M3S_BA_SP_WAVES waves (one wave per task).
-  // M3S_BA_WIDE=t (tests, experiments): every step up to the last one with more than t tasks instead.
+  // the leaf end of the elimination tree: by default the subtree phase below (one launch); with M3S_BA_WIDE or
+  // M3S_BA_FLOW=0 the earlier split into multi-workgroup launches (steps [0, wide_steps)), the root end in the
+  // one-workgroup kernel, minimising the measured step costs (MI355X, C5/C4 graphs): a launch ~5.8 us per step, a
+  // step inside the workgroup ~3.7 us per round of M3S_BA_SP_WAVES waves (one wave per task). M3S_BA_WIDE=t (tests,
+  // experiments): every step up to the last one with more than t tasks.
   std::vector<int> tasks(S.nlev + 1);
   for (int l = 0; l <= S.nlev; l++) {
     const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
@@ -744,12 +755,43 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     if (l < BA_MAX_WIDE_STEPS) Y->step_tasks[l] = tasks[l];
   }
   const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
+  const char* fenv = getenv("M3S_BA_FLOW");
+  const bool flow_on = !(fenv && !strcmp(fenv, "0"));  // M3S_BA_FLOW=0 (A/B experiments): level-synchronous loops
+  std::vector<int> sched, subtab;
   if (const char* w = getenv("M3S_BA_WIDE")) {
     const int thr = atoi(w);
     int last = -1;
     for (int l = 0; l <= S.nlev; l++)
       if (tasks[l] > thr) last = l;
     Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+  } else if (const char* c = getenv("M3S_BA_SUB") && *getenv("M3S_BA_SUB") ? getenv("M3S_BA_SUB") : nullptr;
+             flow_on && !(c != nullptr && atoi(c) < 0)) {
+    // subtree phase (default with the dataflow schedule): steps [0, cut) run as ONE launch, one workgroup per
+    // subtree below the cut; the rest in the one-workgroup kernel. The cut minimises the estimated finish time:
+    // the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor schedule's makespan (the
+    // back substitution does not depend on the cut). M3S_BA_SUB=c (tests, experiments) forces the cut, -1 the
+    // launched wide steps below.
+    int best_cut = 0;
+    if (c != nullptr) {
+      best_cut = std::max(0, std::min(atoi(c), lmax - 1));
+    } else {
+      double best = 1e300;
+      std::vector<int> tmp_s, tmp_t;
+      for (int cut = 0; cut < lmax; cut++) {
+        double sub_us = 0.0;
+        if (cut > 0) ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &tmp_t, &sub_us);
+        const double t = (cut > 0 ? 4.0 + sub_us : 0.0) + ba_flow_schedule(S, 0, M3S_BA_SP_WAVES, &tmp_s, cut);
+        if (t < best - 1e-9) {
+          best = t;
+          best_cut = cut;
+        }
+      }
+    }
+    double sub_us = 0.0;
+    Y->sub_wgs = best_cut > 0 ? ba_subtree_plan(S, best_cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &subtab, &sub_us) : 0;
+    Y->sub_cut = Y->sub_wgs > 0 ? best_cut : 0;
+    if (Y->sub_wgs == 0) subtab.clear();
+    Y->wide_steps = 0;
   } else {
     constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
     std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
@@ -766,18 +808,17 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     }
     Y->wide_steps = best_L;
   }
-  // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h); M3S_BA_FLOW=0 (A/B
-  // experiments): none, the level-synchronous loops run instead
-  std::vector<int> sched;
-  {
-    const char* f = getenv("M3S_BA_FLOW");
-    if (!(f && !strcmp(f, "0"))) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched);
-  }
+  // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
+  if (flow_on) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
   Y->flow = sched.empty() ? 0 : 1;
+  if (!Y->flow && Y->sub_cut > 0) {  // the subtree phase needs the dataflow kernel (it runs the subtrees' spine groups)
+    Y->err = "ba: the subtree phase needs the dataflow schedule";
+    return M3S_EINVAL;
+  }
   const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
                                                    &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
                                                    &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
-                                                   &step_rec};
+                                                   &step_rec, &subtab};
   size_t total = 0;
   for (int k = 0; k < BA_SYM_SECTIONS; k++) {
     Y->off[k] = total;
@@ -858,7 +899,8 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
       (const void**)&a.perm,    (const void**)&a.col_ptr, (const void**)&a.rowL,    (const void**)&a.lev_ptr,
       (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
       (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
-      (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec};
+      (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec,
+      (const void**)&a.sub_tab};
   for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
@@ -866,6 +908,8 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   a.nlev = Y->nlev;
   a.wide_steps = Y->wide_steps;
   a.flow = Y->flow;
+  a.sub_cut = Y->sub_cut;
+  a.sub_wgs = Y->sub_wgs;
   return a;
 }
 
@@ -1266,6 +1310,8 @@ extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   info[5] = P->n_targets;
   info[6] = P->e1 - P->e0;
   info[7] = P->Kp;
+  info[8] = Y->sub_cut;
+  info[9] = Y->sub_wgs;
   return M3S_OK;
 }
 

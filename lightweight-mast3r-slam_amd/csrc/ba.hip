@@ -1073,6 +1073,31 @@ __global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int rec_ba
   else sp_update_group_at(a, T, r0.x, r0.y, r0.z, make_int2(r1.x, r1.y), lane, s_red);
 }
 
+// Subtree phase: steps [0, sub_cut) of the factorisation as ONE launch. Workgroup b owns the subtrees the plan packed
+// into it (ba_pattern.h ba_subtree_plan): per step its factor tasks and the update groups whose targets are its own
+// columns, one wave per task, a workgroup barrier between steps (every hand-off stays on one CU and its XCD's L2).
+// The same per-task code as the wide steps and the one-workgroup kernel: bit-identical factor. The update groups of
+// these steps that target columns above the cut run first in the one-workgroup kernel's dataflow schedule.
+constexpr int SUB_WAVES = 8;
+__global__ void __launch_bounds__(SUB_WAVES * 64) ba_subtree_kernel(BaArgs a) {
+  __shared__ double s_red[SUB_WAVES][64];
+  if (*a.done) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cut = a.sub_cut;
+  const int4* steps = a.sub_tab + (size_t)blockIdx.x * cut;
+  const int4* rec = a.sub_tab + (size_t)a.sub_wgs * cut;
+  const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
+  for (int l = 0; l < cut; l++) {
+    const int4 st = steps[l];
+    for (int t = w; t < st.y; t += SUB_WAVES) {
+      const int4 r0 = rec[2 * (st.x + t)], r1 = rec[2 * (st.x + t) + 1];
+      if (t < st.z) sp_factor_column_at(a, T, r0.x, r0.y, r0.z, r0.w >= 0, make_int2(r1.x, r1.y), lane, s_red[w], a.bad);
+      else sp_update_group_at(a, T, r0.x, r0.y, r0.z, make_int2(r1.x, r1.y), lane, s_red[w]);
+    }
+    if (st.y > 0) __syncthreads();
+  }
+}
+
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
 __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
@@ -1180,7 +1205,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   __syncthreads();
   SPST(3 + 2 * nlev);
-  const bool failed = s_bad != 0 || (a.wide_steps > 0 && *a.bad != 0);
+  const bool failed = s_bad != 0 || ((a.wide_steps > 0 || a.sub_wgs > 0) && *a.bad != 0);
   const bool stalled = (s_bad & BA_BAD_STALL) != 0;
   const int n = a.nb * 7;
   float n2 = 0.0f;
@@ -1264,6 +1289,8 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, const int* step_tasks,
                                           const int* step_base, const int* step_na, hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
+  static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
+  if (a->sub_wgs > 0) hipLaunchKernelGGL(m3s::ba_subtree_kernel, dim3(a->sub_wgs), dim3(m3s::SUB_WAVES * 64), 0, s, *a);
   for (int l = 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],

@@ -262,17 +262,131 @@ struct FlowSim {
 
 }  // namespace
 
-void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched) {
+namespace {
+std::vector<int> col_levels(const BaPattern& P) {
+  std::vector<int> lev(P.nb, 0);
+  for (int l = 0; l < P.nlev; l++)
+    for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) lev[P.lev_col[c]] = l;
+  return lev;
+}
+// estimated task costs (us), shared by the flow schedule and the subtree plan: a factor task ~1.5 + its pull
+// group, an update group ~0.8, ~0.3 per source and 64-row pass (one wave alone on its SIMD issues one fp64
+// instruction per ~3.3 ns)
+inline int col_passes(const BaPattern& P, int j) { return (7 * (P.col_ptr[j + 1] - P.col_ptr[j]) + 1 + 63) / 64; }
+inline int grp_nsrc(const BaPattern& P, int g) { return P.grp[4 * (size_t)g + 2] - P.grp[4 * (size_t)g + 1]; }
+inline double factor_cost(const BaPattern& P, int j) {
+  const int g = P.pull_grp[j];
+  return 1.5 + (g >= 0 ? 0.3 * grp_nsrc(P, g) * col_passes(P, j) : 0.0);
+}
+inline double group_cost(const BaPattern& P, int g) {
+  return 0.8 + 0.3 * grp_nsrc(P, g) * col_passes(P, P.grp[4 * (size_t)g]);
+}
+}  // namespace
+
+int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vector<int>* tab, double* cost_us) {
+  const int nb = P.nb;
+  tab->clear();
+  *cost_us = 0.0;
+  cut = std::min(cut, P.nlev);
+  if (nb <= 0 || cut <= 0) return 0;
+  const std::vector<int> lev = col_levels(P);
+  // subtree root of every column below the cut (parents have higher indices: one downward pass)
+  std::vector<int> root(nb, -1);
+  for (int j = nb - 1; j >= 0; j--) {
+    if (lev[j] >= cut) continue;
+    const int p = P.col_ptr[j + 1] - P.col_ptr[j] > 1 ? P.rowL[P.col_ptr[j] + 1] : -1;
+    root[j] = (p < 0 || lev[p] >= cut) ? j : root[p];
+  }
+  // per subtree and step: its factor tasks and its groups (targets below the cut)
+  std::vector<int> sid(nb, -1), roots;
+  for (int j = 0; j < nb; j++)
+    if (root[j] == j) {
+      sid[j] = (int)roots.size();
+      roots.push_back(j);
+    }
+  const int ns = (int)roots.size();
+  std::vector<std::vector<std::vector<int>>> fac(ns, std::vector<std::vector<int>>(cut)), grp = fac;
+  for (int l = 0; l < cut; l++) {
+    for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
+      const int j = P.lev_col[c];
+      fac[sid[root[j]]][l].push_back(j);
+    }
+    for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
+      const int j = P.grp[4 * (size_t)t];
+      if (lev[j] < cut) grp[sid[root[j]]][l].push_back(t);
+    }
+  }
+  // per-step cost of a set of tasks on `waves` waves (greedy, longest first) + a barrier
+  auto step_cost = [&](const std::vector<double>& c) {
+    if (c.empty()) return 0.0;
+    std::vector<double> w(waves, 0.0), cs = c;
+    std::sort(cs.rbegin(), cs.rend());
+    for (double x : cs) *std::min_element(w.begin(), w.end()) += x;
+    return *std::max_element(w.begin(), w.end()) + 0.3;
+  };
+  std::vector<double> scost(ns, 0.0);
+  for (int s = 0; s < ns; s++)
+    for (int l = 0; l < cut; l++) {
+      std::vector<double> c;
+      for (int j : fac[s][l]) c.push_back(factor_cost(P, j));
+      for (int t : grp[s][l]) c.push_back(group_cost(P, t));
+      scost[s] += step_cost(c);
+    }
+  // pack subtrees into at most max_wg workgroups: longest first onto the least loaded (their steps merge)
+  const int nwg = std::min(ns, std::max(1, max_wg));
+  std::vector<int> order(ns);
+  for (int s = 0; s < ns; s++) order[s] = s;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return scost[a] > scost[b]; });
+  std::vector<double> load(nwg, 0.0);
+  std::vector<std::vector<int>> members(nwg);
+  for (int s : order) {
+    const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[w] += scost[s];
+    members[w].push_back(s);
+  }
+  tab->assign((size_t)nwg * cut * 4, 0);
+  for (int w = 0; w < nwg; w++) {
+    double wc = 0.0;
+    for (int l = 0; l < cut; l++) {
+      int* e = tab->data() + ((size_t)w * cut + l) * 4;
+      const int first = (int)(tab->size() - (size_t)nwg * cut * 4) / 8;
+      int na = 0, nt = 0;
+      std::vector<double> c;
+      auto put = [&](int j, int g) {
+        const int* gq = g >= 0 ? &P.grp[4 * (size_t)g] : nullptr;
+        const int r[8] = {j, P.col_ptr[j], P.col_ptr[j + 1], g, gq ? gq[1] : 0, gq ? gq[2] : 0, 0, 0};
+        tab->insert(tab->end(), r, r + 8);
+        nt++;
+      };
+      for (int s : members[w])
+        for (int j : fac[s][l]) {
+          put(j, P.pull_grp[j]);
+          na++;
+          c.push_back(factor_cost(P, j));
+        }
+      for (int s : members[w])
+        for (int t : grp[s][l]) {
+          put(P.grp[4 * (size_t)t], t);
+          c.push_back(group_cost(P, t));
+        }
+      e = tab->data() + ((size_t)w * cut + l) * 4;  // (the inserts may have moved the table)
+      e[0] = first;
+      e[1] = nt;
+      e[2] = na;
+      wc += step_cost(c);
+    }
+    *cost_us = std::max(*cost_us, wc);
+  }
+  return nwg;
+}
+
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub) {
   const int nb = P.nb, nlev = P.nlev;
   sched->clear();
-  if (nb <= 0) return;
-  std::vector<int> lev(nb, 0);
-  for (int l = 0; l < nlev; l++)
-    for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) lev[P.lev_col[c]] = l;
-  auto nrow = [&](int j) { return 7 * (P.col_ptr[j + 1] - P.col_ptr[j]) + 1; };
-  auto passes = [&](int j) { return (nrow(j) + 63) / 64; };
-  // estimated task costs (us): a factor task ~1.5 + its pull group, an update group ~0.8, ~0.3 per source and
-  // 64-row pass (one wave alone on its SIMD issues one fp64 instruction per ~3.3 ns); hand-off ~0.15
+  if (nb <= 0) return 0.0;
+  const std::vector<int> lev = col_levels(P);
+  const int done_below = std::max(wide, sub);  // columns factored before the one-workgroup kernel starts
+  // estimated task costs (factor_cost / group_cost), hand-off ~0.15 us
   FlowSim F(waves, 0.15);
   std::vector<std::pair<int, int>> tasks;  // {code, q}
   std::vector<int> fac_task(nb, -1), last_grp(nb, -1), napplied(nb, 0), deps;
@@ -283,30 +397,29 @@ void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>*
     }
   };
   for (int l = std::max(0, wide); l <= nlev; l++) {
-    if (l < nlev)
+    if (l < nlev && l >= sub)
       for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
         const int j = P.lev_col[c], g = P.pull_grp[j];
         deps.clear();
         if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
-        double cost = 1.5;
-        if (g >= 0) {
-          src_deps(g);
-          cost += 0.3 * (P.grp[4 * (size_t)g + 2] - P.grp[4 * (size_t)g + 1]) * passes(j);
-        }
+        if (g >= 0) src_deps(g);
         fac_task[j] = (int)tasks.size();
         tasks.push_back({j, napplied[j]});
-        F.place(deps, cost);
+        F.place(deps, factor_cost(P, j));
       }
     for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
       const int j = P.grp[4 * (size_t)t];
+      if (l < sub && lev[j] < sub) continue;  // a subtree's own group: the subtree launch ran it
       deps.clear();
       if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
       src_deps(t);
       last_grp[j] = (int)tasks.size();
       tasks.push_back({-1 - t, napplied[j]++});
-      F.place(deps, 0.8 + 0.3 * (P.grp[4 * (size_t)t + 2] - P.grp[4 * (size_t)t + 1]) * passes(j));
+      F.place(deps, group_cost(P, t));
     }
   }
+  double makespan = 0.0;
+  for (double f : F.fin) makespan = std::max(makespan, f);
   // back substitution: parents first (a parent has the higher index); x_j needs x of struct(j), which the parent's
   // own wait already covered (struct(j) \ {parent} lies in struct(parent))
   FlowSim B(waves, 0.15);
@@ -325,7 +438,7 @@ void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>*
   int* fac_init = bs_ptr + waves + 1;
   int* wl_task = fac_init + nb;
   int* bs_col = wl_task + 2 * (size_t)nt;
-  for (int k = 0; k < nb; k++) fac_init[k] = lev[k] < wide ? 1 : 0;
+  for (int k = 0; k < nb; k++) fac_init[k] = lev[k] < done_below ? 1 : 0;
   for (int w = 0, o = 0, ob = 0; w < waves; w++) {
     wl_ptr[w] = o;
     for (int i = 0; i < nt; i++)
@@ -348,4 +461,5 @@ void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>*
       }
     bs_ptr[w + 1] = ob;
   }
+  return makespan;
 }

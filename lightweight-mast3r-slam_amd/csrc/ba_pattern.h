@@ -61,4 +61,17 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P,
 // the low 24 bits.
 #define BA_BS_NOWAIT (1 << 30)
 #define BA_BS_COL 0xFFFFFF
-void ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched);
+// sub > 0 (subtree phase below, wide = 0): steps [0, sub) belong to the subtree launch except their update groups
+// whose target column sits at level >= sub, which the one-workgroup schedule runs first (in step order per target).
+// Returns the simulated finish time (us) of the factor part (the cost model's estimate).
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub = 0);
+
+// Subtree phase (ba_subtree_kernel, ba.hip): the columns below elimination-tree level `cut` fall into independent
+// subtrees (a column belongs to its highest ancestor below the cut). One workgroup per subtree (small subtrees
+// packed together, at most max_wg workgroups) runs steps [0, cut) of its columns level by level: their factor tasks
+// (each with its pull group) and the update groups whose target is one of its columns; a barrier between steps.
+// Every column's groups still apply in step order, with the same per-task arithmetic: the factor is bit-identical to
+// the level-synchronous schedule. Layout (ints): per workgroup `cut` int4 step entries {first record, tasks, factor
+// tasks (first), 0}, then 8-int task records {j, b0, b1, pull group or -1 (factor task) | group, src begin, src end,
+// 0, 0}. Returns the number of workgroups; *cost_us = the estimated finish time of the slowest workgroup.
+int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vector<int>* tab, double* cost_us);

@@ -63,6 +63,10 @@ struct BaArgs {
   const int* sched;       // dataflow schedule of the one-workgroup part + back substitution (ba_pattern.h)
   int flow;               // sched present (else the level-synchronous loops)
   const int4* step_rec;   // per task of the wide steps, 2 x int4: {j, b0, b1, pull group or -1}, {src begin, end, 0, 0}
+  const int4* sub_tab;    // subtree phase (ba_pattern.h ba_subtree_plan): per workgroup sub_cut step entries, then
+                          // task records (2 x int4, as step_rec)
+  int sub_cut;            // steps [0, sub_cut) run in the subtree launch (0: none)
+  int sub_wgs;            // its workgroups
   const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, sched, staged into LDS by the factor kernel
   int plan_bytes;
   const int* asm_ptr;     // (nL+1) assembly CSR: edge*2 + (sign<0), edge order

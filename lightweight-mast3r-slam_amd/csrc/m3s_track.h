@@ -95,4 +95,8 @@ struct FuseArgs {
   float* Ck_avg;      // (N)   C_out / Nk_new (nullable)
   float* Cf_avg;      // (N)   Cf / Nf (nullable)
   float Nk_new, Nf;
+  int* slot_N;            // keyframe-store slot counters and dirty flag (nullable; m3s_track_fuse_args)
+  int* slot_N_updates;
+  uint8_t* slot_dirty;
+  int N_new, N_updates_new;
 };

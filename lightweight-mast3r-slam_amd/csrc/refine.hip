@@ -42,7 +42,7 @@ typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
 
 #ifdef M3S_REFINE_STATS  // (experiment builds only) per-level deferred lanes / waves
-__device__ unsigned long long g_refine_stats[32];
+__device__ unsigned long long g_refine_stats[64];
 #endif
 #ifdef M3S_REFINE_BSTAMPS  // (experiment builds only) per-block start / end s_memrealtime, hardware id, active lanes
 __device__ unsigned long long g_refine_bstamps[8192 * 4];
@@ -126,41 +126,65 @@ __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, fl
   constexpr int G = 7;
 #pragma unroll
   for (int i = 0; i < G; i++) {
+    // the column's 7 candidate reads in flight together (one LDS latency per column, not per candidate)
+    uint4 c[G];
+#pragma unroll
+    for (int j = 0; j < G; j++) c[j] = base[j * D * RT_COLS + i * D];
 #pragma unroll
     for (int j = 0; j < G; j++) {
-      const uint4 c = base[j * D * RT_COLS + i * D];
-      const h2* cv = reinterpret_cast<const h2*>(&c);
+      const h2* cv = reinterpret_cast<const h2*>(&c[j]);
       float t = a[i * G + j];
 #pragma unroll
       for (int k = 0; k < 4; k++) t = __builtin_amdgcn_fdot2(q4[k], cv[k], t, false);
-      // pin the column's dot products here: otherwise the last chunk's are sunk into the survivor code and
-      // all 49 candidate loads stay live across it (1000+ spilled VGPRs)
-      asm volatile("" : "+v"(t));
       a[i * G + j] = t;
     }
+    // pin the column's dot products here: otherwise the last chunk's are sunk into the survivor code and all 49
+    // candidate loads stay live across it (1000+ spilled VGPRs)
+    float* ac = &a[i * G];
+    asm volatile("" : "+v"(ac[0]), "+v"(ac[1]), "+v"(ac[2]), "+v"(ac[3]), "+v"(ac[4]), "+v"(ac[5]), "+v"(ac[6]));
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// exact c10::Half chains of the survivor mask m in ascending scan order, read from D11h (L2); strict '>'
+// exact c10::Half chains of the survivor mask m in ascending scan order, read from D11h (L2); strict '>'. Two
+// survivors per trip: both candidates' loads are in flight before the first chain (one L2 round trip per pair)
 template <int D, bool PLANAR>
 __device__ __forceinline__ void exact_survivors(const h1* __restrict__ img, int H, int W, const h2* q, int u_lo,
                                                 int v_lo, uint64_t m, h1& max_score, int& bi) {
   while (__ballot(m != 0)) {  // wave-uniform trip count: the lane with the most survivors
-    if (m != 0) {
-      const int c = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int i = c / 7, j = c - 7 * i;
-      uint4 c0, c1, c2;
-      load_chunks<PLANAR>(pix_ptr<PLANAR>(img, (size_t)(v_lo + j * D) * W + (u_lo + i * D)), (size_t)H * W, c0, c1,
-                          c2);
+    const int ca = m != 0 ? __ffsll((long long)m) - 1 : -1;
+    m &= m - 1;
+    const int cb = m != 0 ? __ffsll((long long)m) - 1 : -1;
+    m &= m - 1;
+    uint4 a0, a1, a2, b0, b1, b2;
+    if (ca >= 0) {
+      const int i = ca / 7, j = ca - 7 * i;
+      load_chunks<PLANAR>(pix_ptr<PLANAR>(img, (size_t)(v_lo + j * D) * W + (u_lo + i * D)), (size_t)H * W, a0, a1,
+                          a2);
+    }
+    if (cb >= 0) {
+      const int i = cb / 7, j = cb - 7 * i;
+      load_chunks<PLANAR>(pix_ptr<PLANAR>(img, (size_t)(v_lo + j * D) * W + (u_lo + i * D)), (size_t)H * W, b0, b1,
+                          b2);
+    }
+    if (ca >= 0) {
       h1 sc = (h1)0.0f;
-      add8(sc, &q[0], c0);
-      add8(sc, &q[4], c1);
-      add8(sc, &q[8], c2);
+      add8(sc, &q[0], a0);
+      add8(sc, &q[4], a1);
+      add8(sc, &q[8], a2);
       if (sc > max_score) {
         max_score = sc;
-        bi = c;
+        bi = ca;
+      }
+    }
+    if (cb >= 0) {
+      h1 sc = (h1)0.0f;
+      add8(sc, &q[0], b0);
+      add8(sc, &q[4], b1);
+      add8(sc, &q[8], b2);
+      if (sc > max_score) {
+        max_score = sc;
+        bi = cb;
       }
     }
   }
@@ -275,14 +299,18 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #pragma unroll
     for (int chunk = 0; chunk < F / 8; chunk++) {
       if (chunk) __syncthreads();
+#ifndef RT_NOLOAD
       for (int y = wid; y < nrows; y += 4) {
         const int gy = min(max(wy0 + y, 0), H - 1);
         const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
         __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
       }
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+#ifndef RT_NOCOMP
       if (lane_in) screen_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], a);
+#endif
     }
     if (lane_in) {
       uint64_t vm = (1ull << (G * G)) - 1ull;  // in-image candidates
@@ -304,6 +332,23 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       if (!t.sok) m = ~0ull;
       m &= vm;
       if (!first) m &= ~(1ull << (G * G / 2));
+#ifdef M3S_REFINE_STATS  // survivors per level: lanes' sum [32 + 2D], per-wave maximum summed [33 + 2D]
+      {
+        int ns = __popcll(m), mx = ns;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+        int sm = ns;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off, 64);
+        if (lane == __ffsll((long long)__ballot(1)) - 1) {
+          atomicAdd(&g_refine_stats[32 + 2 * D], (unsigned long long)sm);
+          atomicAdd(&g_refine_stats[33 + 2 * D], (unsigned long long)mx);
+        }
+      }
+#endif
+#ifdef RT_NOSURV
+      m = 0;
+#endif
       int bi = -1;
       exact_survivors<D, PLANAR>(t.img, H, W, q, u_lo, v_lo, m, max_score, bi);
       if (bi >= 0) {
@@ -404,8 +449,15 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
   t.W = W;
   t.lane = threadIdx.x & 63;
   t.wid = threadIdx.x >> 6;
-  t.u_pix = tx * RT_TW + threadIdx.x % RT_TW;
-  t.v_pix = ty * RT_TH + threadIdx.x / RT_TW;
+  {  // pixel of this lane: each ds_read_b128 lane group (16 lanes, one LDS cycle when conflict-free) takes 16
+     // CONTIGUOUS pixels of one row, so lanes whose centres are displaced alike hit 16 distinct bank quads; the
+     // row-major lane order put pixels 17 px apart into one group, which collide on a 1-px displacement change
+    const int l = t.lane & 31;
+    const int g = (l < 4 || (l >= 12 && l < 16) || (l >= 20 && l < 28)) ? 0 : 1;
+    const int r = g == 0 ? (l < 4 ? l : l < 16 ? l - 8 : l - 12) : (l < 12 ? l - 4 : l < 20 ? l - 8 : l - 16);
+    t.u_pix = tx * RT_TW + g * 16 + r;
+    t.v_pix = ty * RT_TH + 2 * t.wid + (t.lane >> 5);
+  }
   t.olist = olist;
   t.ocount = ocount;
   bool active = t.u_pix < W && t.v_pix < H;
@@ -579,9 +631,9 @@ extern "C" int m3s_debug_refine_bstamps(unsigned long long* out) {
 #ifdef M3S_REFINE_STATS
 extern "C" int m3s_debug_refine_stats(unsigned long long* out, int reset) {
   (void)hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_refine_stats), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(m3s::g_refine_stats), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[64] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(m3s::g_refine_stats), z, sizeof(z));
   }
   return 0;

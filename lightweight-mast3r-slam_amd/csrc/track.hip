@@ -716,6 +716,11 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
   if (!solved) return;
   if (f.X_in == nullptr || !(st->status == M3S_TRACK_OK || st->status == M3S_TRACK_MAX_ITERS)) return;
   if (n >= N) return;
+  if (n == 0) {  // the store slot's counters (SharedKeyframes.__setitem__ of the fused record, frame.py:271-289)
+    if (f.slot_N != nullptr) *f.slot_N = f.N_new;
+    if (f.slot_N_updates != nullptr) *f.slot_N_updates = f.N_updates_new;
+    if (f.slot_dirty != nullptr) *f.slot_dirty = 1;
+  }
   float T[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) T[c] = st->T[c];

@@ -54,7 +54,8 @@ class TrackInputs(ctypes.Structure):
 class TrackFuse(ctypes.Structure):
     _fields_ = [("Xk_canon", c_void_p), ("Ck_sum", c_void_p), ("Xkf", c_void_p), ("Ckf", c_void_p),
                 ("Xk_out", c_void_p), ("Ck_out", c_void_p), ("Cf", c_void_p), ("Ck_avg_out", c_void_p),
-                ("Cf_avg_out", c_void_p), ("Nk_new", c_float), ("Nf", c_float)]
+                ("Cf_avg_out", c_void_p), ("Nk_new", c_float), ("Nf", c_float), ("slot_N", c_void_p),
+                ("slot_N_updates", c_void_p), ("slot_dirty", c_void_p), ("N_new", c_int), ("N_updates_new", c_int)]
 
 
 class TrackResult(ctypes.Structure):

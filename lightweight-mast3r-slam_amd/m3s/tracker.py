@@ -17,7 +17,7 @@ import torch
 
 from m3s import _lib
 from m3s.config import config
-from m3s.frame import Frame
+from m3s.frame import Frame, slot_rows
 from m3s.matching import match, match_halves
 from m3s.sim3 import Sim3
 
@@ -118,6 +118,9 @@ class FrameTracker:
         self.device = device
         self.first_chunk = 8  # GN iterations enqueued before the first host readback
         self.last_result = None
+        # fuse straight into a buffer-backed store's slot (SharedKeyframes) instead of tracker.py:101's full-record
+        # copy; False: the reference's copy (A/B tests and the bench's comparison leg)
+        self.slot_writeback = True
         self.reset_idx_f2k()
 
     def reset_idx_f2k(self):
@@ -159,12 +162,17 @@ class FrameTracker:
         # weighted_pointmap on an initialised keyframe is fused on the device (frame.py:74-77); every
         # other filtering mode / an empty keyframe goes through keyframe.update_pointmap
         fuse_fused = cfg["filtering_mode"] == "weighted_pointmap" and keyframe.N > 0
+        # SharedKeyframes (frame.py:220-289): the fusion kernel writes X / C and the slot's N, N_updates, is_dirty
+        # into the slot itself; the rest of the record (img, uimg, feat, pos, T_WC) is what the slot already holds
+        slot = None
+        if fuse_fused and self.slot_writeback:
+            slot = slot_rows(self.keyframes, keyframe, len(self.keyframes) - 1)
 
         res, T_f, T_r = self._run_track(
             idx=idx_f2k, valid=valid_match_k, Xf=frame.X_canon, Cf=frame.C, Nf=frame.N, Qff=Qff,
             Xk=keyframe.X_canon, Ck=keyframe.C, Nk=keyframe.N, Qkf=Qkf, T_WCf=frame.T_WC, T_WCk=keyframe.T_WC,
             use_calib=use_calib, img_size=img_size, K=K,
-            fuse=(keyframe, Xkf, Ckf) if fuse_fused else None)
+            fuse=(keyframe, Xkf, Ckf, slot) if fuse_fused else None)
 
         if res.status == _lib.TRACK_SKIPPED:
             print(f"Skipped frame {frame.frame_id}")
@@ -176,13 +184,14 @@ class FrameTracker:
         # fresh (1, 8) views of this call's output, made before the launch: no copy, no op after the wait
         frame.T_WC = Sim3(T_f)
         T_CkCf = Sim3(T_r)
-        if fuse_fused:  # X/C fused on the device by m3s_track into new tensors (frame.py:74-77)
+        if fuse_fused:  # X/C fused on the device by m3s_track (frame.py:74-77): new tensors, or the slot in place
             keyframe.X_canon, keyframe.C = self._fused
             keyframe.N += 1
             keyframe.N_updates += 1
         else:
             keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf)
-        self.keyframes[len(self.keyframes) - 1] = keyframe
+        if slot is None:  # write back the filtered pointmap (tracker.py:101)
+            self.keyframes[len(self.keyframes) - 1] = keyframe
 
         n = res.N
         match_frac_k = res.n_valid_kf / n
@@ -222,11 +231,14 @@ class FrameTracker:
         fz = _lib.TrackFuse()
         keep = []
         self._fused = self._avg = None
-        if fuse is not None:  # out of place like frame.py:75-76 (earlier holders keep the old tensors)
-            kf, Xkf, Ckf = fuse
+        if fuse is not None:  # out of place like frame.py:75-76 (earlier holders keep the old tensors), or in the slot
+            kf, Xkf, Ckf, slot = fuse
             Xin, Cin = c(kf.X_canon), c(kf.C)
             Xkf_c, Ckf_c = c(Xkf), c(Ckf)
-            Xo, Co = torch.empty_like(Xin), torch.empty_like(Cin)
+            if slot is not None:
+                Xo, Co = slot[0], slot[1]
+            else:
+                Xo, Co = torch.empty_like(Xin), torch.empty_like(Cin)
             Cka, Cfa = torch.empty_like(Cin), torch.empty_like(Cf)
             keep += [Xin, Cin, Xkf_c, Ckf_c]
             self._fused = (Xo, Co)
@@ -234,6 +246,9 @@ class FrameTracker:
             fz = _lib.TrackFuse(Xk_canon=dp(Xin), Ck_sum=dp(Cin), Xkf=dp(Xkf_c), Ckf=dp(Ckf_c), Xk_out=dp(Xo),
                                 Ck_out=dp(Co), Cf=dp(Cf), Ck_avg_out=dp(Cka), Cf_avg_out=dp(Cfa),
                                 Nk_new=float(kf.N + 1), Nf=float(Nf or 1))
+            if slot is not None:
+                fz.slot_N, fz.slot_N_updates, fz.slot_dirty = dp(slot[2]), dp(slot[3]), dp(slot[4])
+                fz.N_new, fz.N_updates_new = int(kf.N) + 1, int(kf.N_updates) + 1
         T_out = torch.empty((2, 1, 8), dtype=torch.float32, device=dev)  # T_WCf | T_CkCf
         T_f, T_r = T_out.unbind(0)
         res = _lib.TrackResult()

@@ -48,9 +48,11 @@ X, D = P["X"].cuda(), P["D"].cuda()
 idx, valid = match(X[:1], X[1:], D[:1], D[1:])
 print("idx checksum", int(idx.sum().item()), "lib", _lib.LIB_PATH)
 if hasattr(lib, "m3s_debug_refine_stats"):
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 64)()
     lib.m3s_debug_refine_stats(buf, 1)
     idx, valid = match(X[:1], X[1:], D[:1], D[1:])
     lib.m3s_debug_refine_stats(buf, 0)
     for d in range(5, 0, -1):
-        print(f"d={d}: outlier lanes {buf[2 * d]}  waves with outliers {buf[2 * d + 1]} / {512 * 512 // 64}")
+        print(f"d={d}: outlier lanes {buf[2 * d]}  waves with outliers {buf[2 * d + 1]} / {512 * 512 // 64}; "
+              f"screen survivors per pixel {buf[32 + 2 * d] / (512 * 512):.3f}, per-wave max (mean) "
+              f"{buf[33 + 2 * d] / (512 * 512 // 64):.3f}")

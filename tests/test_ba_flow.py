@@ -22,13 +22,35 @@ def checker(tmp_path_factory):
     return exe
 
 
-# (K, loop edges per keyframe, seed, wide steps): trajectory-like graphs, a pure chain (one spine), tiny graphs,
-# all-in-workgroup (wide 0) and mostly-launched splits
-CASES = [(256, 3, 1, 31), (256, 3, 2, 0), (256, 3, 3, 15), (64, 2, 4, 5), (2, 0, 1, 0), (3, 0, 1, 0),
-         (300, 5, 9, 40), (128, 0, 1, 3), (97, 1, 7, 200)]
+# (K, loop edges per keyframe, seed, wide steps, subtree cut): trajectory-like graphs, a pure chain (one spine),
+# tiny graphs, all-in-workgroup (wide 0) and mostly-launched splits; the subtree phase at forced cuts and at the
+# plan's cost-model cut (-1)
+CASES = [(256, 3, 1, 31, 0), (256, 3, 2, 0, 0), (256, 3, 3, 15, 0), (64, 2, 4, 5, 0), (2, 0, 1, 0, 0), (3, 0, 1, 0, 0),
+         (300, 5, 9, 40, 0), (128, 0, 1, 3, 0), (97, 1, 7, 200, 0),
+         (256, 3, 1, 0, -1), (256, 3, 2, 0, 12), (64, 2, 4, 0, 30), (2, 0, 1, 0, -1), (3, 0, 1, 0, 1),
+         (128, 0, 1, 0, 20), (97, 1, 7, 0, 200)]
 
 
-@pytest.mark.parametrize("K,loops,seed,wide", CASES)
-def test_flow_schedule_completes_in_order(checker, K, loops, seed, wide):
-    out = subprocess.run([checker, str(K), str(loops), str(seed), str(wide)], capture_output=True, text=True)
+@pytest.mark.parametrize("K,loops,seed,wide,sub", CASES)
+def test_flow_schedule_completes_in_order(checker, K, loops, seed, wide, sub):
+    out = subprocess.run([checker, str(K), str(loops), str(seed), str(wide), str(sub)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("traj", ["chess", "euroc"])
+@pytest.mark.parametrize("sub", [-1, 8, 24])
+def test_subtree_phase_on_trajectory_graphs(checker, tmp_path, traj, sub):
+    """The C5 / C4 trajectory graphs (K = 256, 2028 directed edges; the edge set does not depend on the image size):
+    the subtree phase's workgroup steps and the one-workgroup schedule together factor every column with every
+    update group in step order."""
+    import sys
+
+    sys.path.insert(0, os.path.join(REPO, "lightweight-mast3r-slam_amd"))
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
+
+    G = make_traj_graph((chess_poses if traj == "chess" else euroc_poses)(256), 24, 32, seed=1)
+    f = tmp_path / "edges.txt"
+    f.write_text("".join(f"{a} {b}\n" for a, b in zip(G["ii"].tolist(), G["jj"].tolist())))
+    out = subprocess.run([checker, "-f", str(f), "0", str(sub)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
+    assert " sub 0 " not in out.stdout, out.stdout  # these graphs do get a subtree phase

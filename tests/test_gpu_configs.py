@@ -8,7 +8,7 @@
   at reduced N (48x64, two-way edges, E_dir ~2000) in rays and calib mode, against the fp64 truth
   (O.gauss_newton_f64) at 1e-5 — this runs the whole block-sparse solve of a 255-pose system end to end.
 
-Tolerances: idx/valid mismatch rate <= 1e-3 (SURVEY a-note 4: `.long()` of a p_new within rounding distance of
+Tolerances: idx/valid mismatch rate <= 1e-4 (SURVEY a-note 4: `.long()` of a p_new within rounding distance of
 an integer; the observed rate is printed), poses 1e-5, fused points 1e-5 absolute + 1e-5 relative.
 """
 import numpy as np
@@ -96,7 +96,7 @@ def test_track_at_config_size_matches_oracle(cfg, H, W, mode, K):
     print(f"{cfg} {H}x{W} {mode}: idx mismatch {mis_idx:.2e}, valid mismatch {mis_valid:.2e}, "
           f"GN iters gpu {g_it} / oracle {r_it}, pose err {np.abs(g_T - r_T).max():.2e}, "
           f"kf X err {np.abs(g_kX - r_kX).max():.2e}")
-    assert mis_idx <= 1e-3 and mis_valid <= 1e-3
+    assert mis_idx <= 1e-4 and mis_valid <= 1e-4
     assert g_it == r_it
     np.testing.assert_allclose(g_T, r_T, atol=1e-5)
     np.testing.assert_allclose(g_kX, r_kX, atol=1e-5, rtol=1e-5)
@@ -117,8 +117,8 @@ def test_match_warm_start_at_c1_matches_oracle():
     g_idx, g_valid = match(Xd[:1], Xd[1:], Dd[:1], Dd[1:], idx_1_to_2_init=torch.from_numpy(init).cuda())
     mis = float((g_idx.cpu().numpy() != r_idx).mean())
     print(f"C1 warm start: idx mismatch {mis:.2e}")
-    assert mis <= 1e-3
-    assert float((g_valid.cpu().numpy() != r_valid).mean()) <= 1e-3
+    assert mis <= 1e-4
+    assert float((g_valid.cpu().numpy() != r_valid).mean()) <= 1e-4
 
 
 def test_batched_symmetric_match_at_c3_size_matches_oracle():
@@ -143,7 +143,7 @@ def test_batched_symmetric_match_at_c3_size_matches_oracle():
         mis = float((g_idx[b] != r_idx[b]).mean())
         mis_v = float((g_valid[b] != r_valid[b]).mean())
         print(f"C3 batched match row {b}: idx mismatch {mis:.2e}, valid mismatch {mis_v:.2e}")
-        assert mis <= 1e-3 and mis_v <= 1e-3
+        assert mis <= 1e-4 and mis_v <= 1e-4
 
 
 SIG = {"rays": (0.003, 10.0), "calib": (1.0, 10.0)}
@@ -202,12 +202,13 @@ def test_ba_k256_graph_vs_fp64_truth(request, mode, traj, solver, monkeypatch):
 
 
 def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
-    """The block-sparse factorisation's two schedules — wide elimination-tree steps as multi-workgroup launches
-    (default: the plan's cost-model split; M3S_BA_WIDE=t: every step up to the last one wider than t tasks, 0: every
-    step) or all steps inside one
-    workgroup (M3S_BA_WIDE huge) — run the same per-task arithmetic in the same order: poses and dx must be
-    bit-identical on the K=256 chess graph. Each split runs with the one-workgroup part on its dataflow schedule
-    (default) and level-synchronous (M3S_BA_FLOW=0): the per-column update order is the same, so bit-identical too."""
+    """The block-sparse factorisation's schedules run the same per-task arithmetic in the same per-column order, so
+    poses and dx must be bit-identical on the K=256 chess graph:
+      * the subtree phase (default; ba_subtree_kernel: one launch, one workgroup per elimination subtree below a cut,
+        the rest in one workgroup) at the plan's cost-model cut and at forced cuts (M3S_BA_SUB=c);
+      * wide elimination-tree steps as multi-workgroup launches (M3S_BA_SUB=-1: the launch-cost model's split;
+        M3S_BA_WIDE=t: every step up to the last one wider than t tasks, 0: every step, huge: all steps inside one
+        workgroup), each with the one-workgroup part on its dataflow schedule and level-synchronous (M3S_BA_FLOW=0)."""
     import mast3r_slam_backends as B
 
     G = chess_graph
@@ -215,18 +216,71 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
     c = lambda a, dt=None: (torch.from_numpy(np.ascontiguousarray(a)) if dt is None
                             else torch.from_numpy(np.ascontiguousarray(a)).to(dt)).cuda()
     args = (c(G["Xs"]), c(G["Cs"]), c(G["ii"]), c(G["jj"]), c(G["idx"]), c(G["valid"], torch.bool), c(G["Q"]))
-    out = {}
+
+    def run(env):
+        for k in ("M3S_BA_FLOW", "M3S_BA_WIDE", "M3S_BA_SUB"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        T = c(G["Twc0"])
+        dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
+        return T.cpu().numpy(), dx.cpu().numpy()
+
+    envs = [{}, {"M3S_BA_SUB": "8"}, {"M3S_BA_SUB": "24"}, {"M3S_BA_SUB": "1"}]
     for flow in ("1", "0"):
-        monkeypatch.setenv("M3S_BA_FLOW", flow)
-        for wide in ("1000000", "16", "0", "default"):
-            if wide == "default":  # the plan's cost-model split
-                monkeypatch.delenv("M3S_BA_WIDE", raising=False)
-            else:
-                monkeypatch.setenv("M3S_BA_WIDE", wide)
-            T = c(G["Twc0"])
-            dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
-            out[(flow, wide)] = (T.cpu().numpy(), dx.cpu().numpy())
-    ref = out[("0", "1000000")]
-    for key, (T, dx) in out.items():
-        assert np.array_equal(T, ref[0]), f"poses differ with M3S_BA_FLOW, M3S_BA_WIDE = {key}"
-        assert np.array_equal(dx, ref[1]), f"dx differs with M3S_BA_FLOW, M3S_BA_WIDE = {key}"
+        envs += [{"M3S_BA_FLOW": flow, "M3S_BA_SUB": "-1"}]
+        envs += [{"M3S_BA_FLOW": flow, "M3S_BA_WIDE": w} for w in ("1000000", "16", "0")]
+    ref = run({"M3S_BA_FLOW": "0", "M3S_BA_WIDE": "1000000"})
+    for env in envs:
+        T, dx = run(env)
+        assert np.array_equal(T, ref[0]), f"poses differ with {env}"
+        assert np.array_equal(dx, ref[1]), f"dx differs with {env}"
+
+
+# The timed BA workloads at their full keyframe resolution (main.py:150-155 solves at the keyframes' own size):
+# C5 = 7-Scenes chess, 384x512 calib; the ETH3D half of C5 = 304x512 calib (ETH3D ground truth is not in the
+# reference, so the chess trajectory carries the ETH3D image shape); C4 = EuRoC MH_02, 320x512 rays. 2 GN iterations
+# with the early exit off, against the oracle's fp64 truth (the checker only) at SURVEY a-note 6's 1e-5. Every edge
+# then spans ~8 linearisation chunks of 24,576 points, the bench's exact chunking.
+FULL_CASES = [("C5-chess", "chess", 384, 512, "calib"), ("C5-eth3d", "chess", 304, 512, "calib"),
+              ("C4-euroc", "euroc", 320, 512, "rays")]
+
+
+@pytest.mark.parametrize("case,traj,H,W,mode", FULL_CASES, ids=[c[0] for c in FULL_CASES])
+def test_ba_k256_full_resolution_vs_fp64_truth(case, traj, H, W, mode):
+    import mast3r_slam_backends as B
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
+
+    G = make_traj_graph((chess_poses if traj == "chess" else euroc_poses)(256), H, W, seed=1, device="cuda")
+    d = {k: v for k, v in G.items() if torch.is_tensor(v)}
+    Xs = d["Xs"]
+    if mode == "calib":
+        from m3s.geometry import constrain_points_to_ray
+
+        Xs = constrain_points_to_ray((H, W), Xs, d["K"]).contiguous()
+    sa, sb = SIG[mode]
+    iters = 2
+    T = d["Twc0"].clone()
+    if mode == "rays":
+        dx = B.gauss_newton_rays(T, Xs, d["Cs"], d["ii"], d["jj"], d["idx"], d["valid"], d["Q"], sa, sb, 0.0, 1.5,
+                                 iters, 0.0)[0]
+    else:
+        dx = B.gauss_newton_calib(T, Xs, d["Cs"], d["K"], d["ii"], d["jj"], d["idx"], d["valid"], d["Q"], H, W, -10,
+                                  1e-6, sa, sb, 0.0, 1.5, iters, 0.0)[0]
+    T, dx = T.cpu().numpy(), dx.cpu().numpy()
+    n = lambda t: t.cpu().numpy()
+    Xs_np = n(Xs)
+    del Xs
+    h = {k: n(v) for k, v in d.items()}
+    del d, G
+    torch.cuda.empty_cache()
+    p = O.ba_params(mode, sa, sb, 0.0, 1.5, K=h["K"], height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    O.set_threads(16)
+    T_ref, dx_ref, _ = O.gauss_newton_f64(mode, h["Twc0"], Xs_np, h["Cs"][..., 0], h["ii"], h["jj"], h["idx"],
+                                          h["valid"][..., 0], h["Q"][..., 0], p, iters, 0.0)
+    err = np.abs(T - T_ref).max()
+    print(f"{case} K=256 {H}x{W} {mode}, {h['ii'].shape[0]} edges, {iters} iterations: pose err vs fp64 truth "
+          f"{err:.2e}, dx err {np.abs(dx - dx_ref).max():.2e}")
+    assert dx.shape == (255, 7)
+    np.testing.assert_allclose(T, T_ref, atol=1e-5)
+    np.testing.assert_allclose(dx, dx_ref, atol=1e-5)

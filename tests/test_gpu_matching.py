@@ -1,7 +1,7 @@
 """GPU parity: matching kernels (iter_proj, refine_matches, fused match) vs the oracle / golden vectors.
 
 Tolerances: p_new within 1e-4 px (FMA/ordering), `converged` and integer
-indices bit-exact except for documented near-integer truncation flips (<= 1e-3 of pixels).
+indices bit-exact except for documented near-integer truncation flips (<= 1e-4 of pixels, SURVEY a-note 4).
 """
 import numpy as np
 import pytest
@@ -97,11 +97,11 @@ def test_fused_match_matches_golden(golden):
     g = golden("matching_48x64.npz")
     idx, valid = match(_dev(g["X11"]), _dev(g["X21"]), _dev(g["D11"]), _dev(g["D21"]))
     assert idx.shape == (1, 48 * 64) and valid.shape == (1, 48 * 64, 1)
-    assert (idx.cpu().numpy() != g["idx"]).mean() <= 1e-3
-    assert (valid.cpu().numpy() != g["valid"]).mean() <= 1e-3
+    assert (idx.cpu().numpy() != g["idx"]).mean() <= 1e-4
+    assert (valid.cpu().numpy() != g["valid"]).mean() <= 1e-4
     idx_w, valid_w = match(_dev(g["X11"]), _dev(g["X21"]), _dev(g["D11"]), _dev(g["D21"]), _dev(g["idx_init"]))
-    assert (idx_w.cpu().numpy() != g["idx_warm"]).mean() <= 1e-3
-    assert (valid_w.cpu().numpy() != g["valid_warm"]).mean() <= 1e-3
+    assert (idx_w.cpu().numpy() != g["idx_warm"]).mean() <= 1e-4
+    assert (valid_w.cpu().numpy() != g["valid_warm"]).mean() <= 1e-4
 
 
 @pytest.mark.parametrize("shape", [(96, 128, 2), (128, 160, 1)])
@@ -117,8 +117,8 @@ def test_fused_match_vs_oracle_batched(shape):
     D21 = np.stack([p["D"][1].numpy() for p in Ps])
     ref_idx, ref_valid = O.match(X11, X21, D11, D21)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-3
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
+    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
+    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
 
 
 @pytest.mark.parametrize("shape,dmax", [((2, 50, 70), 5), ((1, 40, 96), 3), ((1, 64, 64), 8), ((1, 33, 47), 1)])
@@ -137,8 +137,8 @@ def test_fused_match_ragged_and_dilations_vs_oracle(shape, dmax):
     D21 = np.stack([p["D"][1].numpy() for p in Ps])
     ref_idx, ref_valid = O.match(X11, X21, D11, D21, dilation_max=dmax)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-3
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
+    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
+    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
 
 
 def test_fused_match_scattered_warm_start_vs_oracle():
@@ -155,8 +155,8 @@ def test_fused_match_scattered_warm_start_vs_oracle():
     init = np.random.default_rng(3).integers(0, H * W, size=(1, H * W)).astype(np.int64)
     ref_idx, ref_valid = O.match(X11, X21, D11, D21, idx_init=init)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21), _dev(init))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-3
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-3
+    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
+    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
     # reference op on the same scattered centres: bit-exact c10::Half refine
     rays, pts, p_init = O.prep_for_iter_proj(X11, X21, init)
     p_new, _ = O.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)

@@ -224,3 +224,76 @@ def test_track_while_ba_runs_on_another_stream():
     for a, b in zip(solo, both):
         assert (a == b) if isinstance(a, int) else torch.equal(a, b)
     assert torch.equal(T_ba, T_ba_solo) and torch.equal(dx_ba, dx_ba_solo)
+
+
+def _shared_store(P, H, W, manager):
+    """A SharedKeyframes (the reference's multi-process store, frame.py:220-327) holding one keyframe record."""
+    from m3s.frame import Frame, SharedKeyframes
+    from m3s.sim3 import Sim3
+
+    kfs = SharedKeyframes(manager, H, W, buffer=4, device="cuda", feat_dim=64)
+    kf = Frame(0, (H, W), T_WC=Sim3.Identity(1, device="cuda"))
+    kf.K = P["K"].cuda()
+    kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
+    g = torch.Generator().manual_seed(3)
+    kf.img = torch.rand(3, H, W, generator=g).cuda()
+    kf.uimg = torch.rand(H, W, 3, generator=g)
+    kf.img_shape = torch.tensor([[H, W]], dtype=torch.int).cuda()
+    kf.img_true_shape = kf.img_shape.clone()
+    kf.feat = torch.rand(1, H * W // 256, 64, generator=g).cuda()
+    kf.pos = torch.randint(0, 100, (1, H * W // 256, 2), generator=g).cuda()
+    kfs.append(kf)
+    kfs.set_intrinsics(P["K"].cuda())
+    kfs.get_dirty_idx()  # clean
+    return kfs
+
+
+def test_track_writes_fused_keyframe_into_shared_slot():
+    """SURVEY §8f row 2 (keyframe-buffer write-back): with a SharedKeyframes store the fused tracker writes the fused
+    X / C and the slot's N, N_updates, is_dirty straight into the slot (fusion kernel, in place) instead of
+    tracker.py:101's full-record __setitem__ copy (frame.py:271-289). Over several tracked frames every buffer of the
+    store is bit-identical to the reference's full-copy path (slot_writeback = False), and so are the poses and
+    the returned match_info."""
+    import multiprocessing as mp
+
+    from m3s.config import config
+    from m3s.frame import Frame
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    config["use_calib"] = True
+    config["tracking"]["filtering_mode"] = "weighted_pointmap"
+    H, W = 64, 96
+    pairs = [make_pair(H, W, seed=s) for s in (11, 12, 13)]
+    manager = mp.get_context("spawn").Manager()
+    try:
+        out = {}
+        for direct in (True, False):
+            kfs = _shared_store(pairs[0], H, W, manager)
+            tr = FrameTracker(SyntheticModel(pairs, "cuda"), kfs, "cuda")
+            tr.slot_writeback = direct
+            poses, infos = [], []
+            for f in range(5):
+                frame = Frame(1 + f, (H, W), T_WC=Sim3.Identity(1, device="cuda"))
+                new_kf, info, reloc = tr.track(frame)
+                assert not reloc
+                poses.append(frame.T_WC.data.cpu().clone())
+                infos.append([t.cpu().clone() for t in info])
+            torch.cuda.synchronize()
+            bufs = {k: getattr(kfs, k).cpu().clone() for k in ("dataset_idx", "img", "uimg", "img_shape",
+                                                                   "img_true_shape", "T_WC", "X", "C", "N",
+                                                                   "N_updates", "feat", "pos", "is_dirty")}
+            out[direct] = (bufs, poses, infos, len(kfs))
+        a, b = out[True], out[False]
+        assert a[3] == b[3] == 1
+        for k in a[0]:
+            assert torch.equal(a[0][k], b[0][k]), f"slot buffer {k} differs"
+        assert int(a[0]["N"][0]) == 6 and int(a[0]["N_updates"][0]) == 6 and bool(a[0]["is_dirty"][0])
+        for pa, pb in zip(a[1], b[1]):
+            assert torch.equal(pa, pb)
+        for ia, ib in zip(a[2], b[2]):
+            assert all(torch.equal(x, y) for x, y in zip(ia, ib))
+    finally:
+        manager.shutdown()
+        config["use_calib"] = False
