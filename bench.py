@@ -142,6 +142,49 @@ def bench_tracking(args, rank, world, dev):
     return elapsed, kern, float(np.mean(iters)), H * W, step_s
 
 
+def bench_configs(args, dev, frames=60, warmup=10):
+    """Per-config tracking throughput at each config's own shape, beside the headline C2-shaped
+    512x512 line: C1 = one 512x512 synthetic pair, rays (base config), exactly 5 GN iterations (convergence tests
+    off); C2 = TUM fr1_room, 512x384 calib, GN to convergence. Host-stamped per-frame wall, median and frames/s."""
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    out = {}
+    for name, H, W, calib, fixed in (("C1", 512, 512, False, 5), ("C2", 384, 512, True, None)):
+        config["use_calib"] = calib
+        saved = dict(config["tracking"])
+        if fixed:
+            config["tracking"].update(max_iters=fixed, rel_error=0.0, delta_norm=0.0)
+        try:
+            pairs = [make_pair(H, W, seed=700 + r) for r in range(args.ring)]
+            model = SyntheticModel(pairs, dev)
+            kf = Frame(0, (H, W), T_WC=Sim3.Identity(1, device=dev))
+            kf.K = pairs[0]["K"].to(dev)
+            kf.update_pointmap(pairs[0]["Xk"].to(dev), pairs[0]["Ck"].to(dev))
+            kfs = Keyframes()
+            kfs.append(kf)
+            tr = FrameTracker(model, kfs, dev)
+            st, its = [], []
+            for i in range(warmup + frames):
+                t0 = time.perf_counter()
+                _, _, reloc = tr.track(Frame(i + 1, (H, W), T_WC=kf.T_WC))
+                st.append(time.perf_counter() - t0)
+                its.append(tr.last_result.iters)
+                assert not reloc, "synthetic tracking failed"
+            torch.cuda.synchronize()
+            med = float(np.median(st[warmup:]))
+            out[name] = {"frames_per_s": 1.0 / med, "median_ms": med * 1e3, "shape": [H, W],
+                         "mode": "calib" if calib else "rays", "gn_iters_mean": float(np.mean(its[warmup:]))}
+        finally:
+            config["tracking"].clear()
+            config["tracking"].update(saved)
+    config["use_calib"] = args.mode == "calib"
+    return out
+
+
 def bench_store(args, dev, frames=60, warmup=10):
     """tracking through the reference's multi-process keyframe store (m3s.frame.SharedKeyframes =
     frame.py:220-327: share_memory_ buffers behind a Manager RLock, 512x512, the reference's 1024-dim feat / pos
@@ -244,7 +287,11 @@ def pmc_traffic(name, pattern="r[0-9][0-9]_pmc.json"):
 
 # SURVEY.md §8(d) BA legs: C5 = 256-keyframe chess graph, calib, 512x384 (7-Scenes shape); C4 = EuRoC-shaped
 # graph (MH_02_easy trajectory), rays (eval_no_calib), 512x320
-BA_LEGS = {"C5": dict(traj="chess", mode="calib", H=384, W=512), "C4": dict(traj="euroc", mode="rays", H=320, W=512)}
+# C5 = 7-Scenes chess (384x512 calib) + ETH3D (512x304 calib; its ground truth is not in the reference, so the chess
+# trajectory carries the ETH3D image shape); C4 = EuRoC MH_02 (320x512 rays)
+BA_LEGS = {"C5": dict(traj="chess", mode="calib", H=384, W=512), "C4": dict(traj="euroc", mode="rays", H=320, W=512),
+           "C5e": dict(traj="chess", mode="calib", H=304, W=512)}
+BA_PMC_TAG = {"C5": "_ba", "C4": "_ba_c4", "C5e": "_ba_eth3d"}
 # Compulsory HBM bytes of the build's BA loop. Once per call the pack streams, per point and edge,
 # valid 1 + idx 8 + Q 4 in and the 16-B record out (29 B), and gathers from the keyframes' X (12 B) and C (4 B),
 # compulsory once per keyframe point. Every GN iteration then streams only the 16-B record of each point of each
@@ -326,8 +373,7 @@ def bench_ba(args, rank, world, dev, leg):
     lin_s = spans["ba_linearize"] * 1e-3
     n_e = e1 - e0
     alg = n_e * N * BA_REC_BYTES + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
-    pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}>",
-                    pattern=f"r[0-9][0-9]_ba{'_c4' if leg == 'C4' else ''}_pmc.json")
+    pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}>", pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     traffic = pmc["traffic_bytes"] if pmc else None
     roof = {"kernel": "ba_lin_kernel + ba_edge_kernel", "bound": "hbm", "achieved": alg / lin_s / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / lin_s / 1e9 / HBM_PEAK_GBS,
@@ -661,8 +707,10 @@ def main():
     if not args.no_ba:
         ba = bench_ba(args, rank, world, dev, "C5")
         ba["c4"] = bench_ba(args, rank, world, dev, "C4")
+        ba["eth3d"] = bench_ba(args, rank, world, dev, "C5e")
     retrieval = bench_retrieval(dev) if (rank == 0 and not args.no_retrieval) else None
     store = bench_store(args, dev) if (rank == 0 and not args.no_store) else None
+    configs = bench_configs(args, dev) if (rank == 0 and not args.no_store) else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
@@ -682,7 +730,7 @@ def main():
                        "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
             "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,
-            "retrieval": retrieval, "store": store,
+            "retrieval": retrieval, "store": store, "configs": configs,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

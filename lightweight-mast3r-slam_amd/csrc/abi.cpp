@@ -540,6 +540,7 @@ inline size_t ba_max_blocks(int Kp) {
 constexpr int BA_SYM_SECTIONS = 17;  // the symbolic half's sections (build_symbolic)
 constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
 constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
+constexpr int BA_SP_PLAN_BYTES = 144 * 1024;  // ba.hip SP_PLAN_BYTES: LDS of the one-workgroup factor kernel
 constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
@@ -758,41 +759,20 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   const char* fenv = getenv("M3S_BA_FLOW");
   const bool flow_on = !(fenv && !strcmp(fenv, "0"));  // M3S_BA_FLOW=0 (A/B experiments): level-synchronous loops
   std::vector<int> sched, subtab;
-  if (const char* w = getenv("M3S_BA_WIDE")) {
-    const int thr = atoi(w);
-    int last = -1;
-    for (int l = 0; l <= S.nlev; l++)
-      if (tasks[l] > thr) last = l;
-    Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
-  } else if (const char* c = getenv("M3S_BA_SUB") && *getenv("M3S_BA_SUB") ? getenv("M3S_BA_SUB") : nullptr;
-             flow_on && !(c != nullptr && atoi(c) < 0)) {
-    // subtree phase (default with the dataflow schedule): steps [0, cut) run as ONE launch, one workgroup per
-    // subtree below the cut; the rest in the one-workgroup kernel. The cut minimises the estimated finish time:
-    // the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor schedule's makespan (the
-    // back substitution does not depend on the cut). M3S_BA_SUB=c (tests, experiments) forces the cut, -1 the
-    // launched wide steps below.
-    int best_cut = 0;
-    if (c != nullptr) {
-      best_cut = std::max(0, std::min(atoi(c), lmax - 1));
-    } else {
-      double best = 1e300;
-      std::vector<int> tmp_s, tmp_t;
-      for (int cut = 0; cut < lmax; cut++) {
-        double sub_us = 0.0;
-        if (cut > 0) ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &tmp_t, &sub_us);
-        const double t = (cut > 0 ? 4.0 + sub_us : 0.0) + ba_flow_schedule(S, 0, M3S_BA_SP_WAVES, &tmp_s, cut);
-        if (t < best - 1e-9) {
-          best = t;
-          best_cut = cut;
-        }
-      }
-    }
-    double sub_us = 0.0;
-    Y->sub_wgs = best_cut > 0 ? ba_subtree_plan(S, best_cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &subtab, &sub_us) : 0;
-    Y->sub_cut = Y->sub_wgs > 0 ? best_cut : 0;
-    if (Y->sub_wgs == 0) subtab.clear();
-    Y->wide_steps = 0;
-  } else {
+  // bytes the one-workgroup dataflow kernel stages in LDS for a schedule (m3s_launch_ba_solve's test): the loop
+  // tables col_ptr .. sidx (sections 1-9, 16-B aligned as packed below) + the schedule, x (8 doubles per column) and
+  // 3 flags per column. A plan whose dataflow schedule does not fit runs level-synchronously (no subtree phase).
+  size_t table_bytes = 0;
+  {
+    const std::vector<int>* t[9] = {&S.col_ptr, &S.lev_ptr, &S.lev_col, &S.grp_ptr, &S.grp, &S.pull_grp, &S.src,
+                                    &S.sidx, &S.rowL};
+    for (const std::vector<int>* v : t) table_bytes += (sizeof(int) * v->size() + 15) & ~(size_t)15;
+  }
+  auto flow_fits = [&](const std::vector<int>& sc) {
+    const size_t plan = table_bytes + sizeof(int) * sc.size();
+    return ((plan + 15) & ~(size_t)15) + (size_t)S.nb * 64 + (size_t)S.nb * 12 <= (size_t)BA_SP_PLAN_BYTES;
+  };
+  auto legacy_split = [&]() {  // launched wide steps: minimise the measured step costs
     constexpr double kLaunchUs = 5.8, kRoundUs = 3.7;
     std::vector<double> suffix(lmax + 1, 0.0);  // cost of steps [L, lmax) inside the workgroup
     for (int l = lmax - 1; l >= 0; l--)
@@ -806,11 +786,53 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
         best_L = L;
       }
     }
-    Y->wide_steps = best_L;
+    return best_L;
+  };
+  const char* senv = getenv("M3S_BA_SUB");
+  if (senv != nullptr && *senv == '\0') senv = nullptr;
+  if (const char* w = getenv("M3S_BA_WIDE")) {
+    const int thr = atoi(w);
+    int last = -1;
+    for (int l = 0; l <= S.nlev; l++)
+      if (tasks[l] > thr) last = l;
+    Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
+  } else if (flow_on && !(senv != nullptr && atoi(senv) < 0)) {
+    // subtree phase (default with the dataflow schedule): steps [0, cut) run as ONE launch, one workgroup per
+    // subtree below the cut; the rest in the one-workgroup kernel. The cut minimises the estimated finish time:
+    // the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor schedule's makespan (the
+    // back substitution does not depend on the cut), among the cuts whose schedule fits the kernel's LDS.
+    // M3S_BA_SUB=c (tests, experiments) forces the cut, -1 the launched wide steps below.
+    std::vector<std::pair<double, int>> cand;
+    std::vector<int> tmp_t;
+    for (int cut = 0; cut < lmax; cut++) {
+      if (senv != nullptr && cut != std::max(0, std::min(atoi(senv), lmax - 1))) continue;
+      double sub_us = 0.0;
+      if (cut > 0) ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &tmp_t, &sub_us);
+      std::vector<int> sc;
+      const double t = (cut > 0 ? 4.0 + sub_us : 0.0) + ba_flow_schedule(S, 0, M3S_BA_SP_WAVES, &sc, cut);
+      if (flow_fits(sc)) cand.push_back({t, cut});
+    }
+    std::stable_sort(cand.begin(), cand.end());
+    if (cand.empty()) {  // no dataflow schedule fits: level-synchronous with launched wide steps
+      Y->wide_steps = legacy_split();
+    } else {
+      const int cut = cand[0].second;
+      double sub_us = 0.0;
+      Y->sub_wgs = cut > 0 ? ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &subtab, &sub_us) : 0;
+      Y->sub_cut = Y->sub_wgs > 0 ? cut : 0;
+      if (Y->sub_wgs == 0) subtab.clear();
+      Y->wide_steps = 0;
+    }
+  } else {
+    Y->wide_steps = legacy_split();
   }
   // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
   if (flow_on) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
   Y->flow = sched.empty() ? 0 : 1;
+  if (Y->flow && !flow_fits(sched)) {  // the kernel would run level-synchronously: drop the schedule (and say so)
+    Y->flow = 0;
+    sched.clear();
+  }
   if (!Y->flow && Y->sub_cut > 0) {  // the subtree phase needs the dataflow kernel (it runs the subtrees' spine groups)
     Y->err = "ba: the subtree phase needs the dataflow schedule";
     return M3S_EINVAL;

@@ -1290,14 +1290,18 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
                                           const int* step_base, const int* step_na, hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
   static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
+  // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column
+  const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64;
+  const bool flow_fits = a->flow && lds + (size_t)a->nb * 12 <= (size_t)m3s::SP_PLAN_BYTES;
+  // the subtree phase leaves the spine-targeted groups of its steps to the dataflow schedule (the plan only builds
+  // one when that schedule fits: a level-synchronous run would re-factor the subtrees' columns)
+  if (a->sub_wgs > 0 && !flow_fits) return hipErrorInvalidValue;
   if (a->sub_wgs > 0) hipLaunchKernelGGL(m3s::ba_subtree_kernel, dim3(a->sub_wgs), dim3(m3s::SUB_WAVES * 64), 0, s, *a);
   for (int l = 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],
                          step_na[l]);
-  // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column
-  const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64;
-  if (a->flow && lds + (size_t)a->nb * 12 <= (size_t)m3s::SP_PLAN_BYTES)
+  if (flow_fits)
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else if (lds <= (size_t)m3s::SP_PLAN_BYTES) {
     BaArgs b = *a;

@@ -96,6 +96,13 @@ static inline uint16_t m3o_f2h(float f) {
 /* host threads of the OpenMP loops (bench.py's cpu_baseline times 1 thread and all cores) */
 void m3o_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
+/* BA sums in the reference's own order (gn_kernels.cu:531-723, 890-1138, 1326-1543): per edge THREADS = 256
+ * float accumulators, point k into thread k % 256 (each thread walks k = tid, tid + 256, ...), every product-sum
+ * contracted to an FMA as nvcc does by default (hij += w * Jn * Jm -> fmaf(w * Jn, Jm, hij)), then the float
+ * blockReduce tree (:45-55: +128, +64, +32, ..., +1). 0 (default): per-point fp32 products summed in fp64. */
+static int g_ref_order = 0;
+void m3o_set_ref_order(int on) { g_ref_order = on; }
+
 void m3o_f32_to_f16(const float* in, uint16_t* out, int64_t n) {
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; i++) out[i] = m3o_f2h(in[i]);
@@ -503,6 +510,23 @@ static void m3o_accum_row(double* hij, double* vi, double* vj, const float* Jx, 
   }
 }
 
+static void m3o_accum_row_f(float* hij, float* vi, float* vj, const float* Jx, float w, float err) {
+  int l = 0;
+  for (int n = 0; n < 14; n++)
+    for (int m = 0; m <= n; m++, l++) hij[l] = fmaf(w * Jx[n], Jx[m], hij[l]);
+  for (int n = 0; n < 7; n++) {
+    vi[n] = fmaf(w * err, Jx[n], vi[n]);
+    vj[n] = fmaf(w * err, Jx[7 + n], vj[n]);
+  }
+}
+
+/* blockReduce (gn_kernels.cu:36-55) of 256 float slots with stride `st` (slot t at v[t * st]) -> v[0] */
+static float m3o_block_reduce(float* v, int st) {
+  for (int h = 128; h >= 1; h >>= 1)
+    for (int t = 0; t < h; t++) v[t * st] += v[(t + h) * st];
+  return v[0];
+}
+
 static void m3o_row(const float* Ji_local, const float* ti, const float* qi, const float* si, float* Jx) {
   float Jl[7];
   memcpy(Jl, Ji_local, sizeof(Jl));
@@ -523,6 +547,17 @@ static void m3o_linearize_edge(const m3o_ba_params* P, const float* Twc, const f
   memset(hij, 0, sizeof(hij));
   memset(vi, 0, sizeof(vi));
   memset(vj, 0, sizeof(vj));
+  /* reference order: per thread slot t (0..255) 105 + 7 + 7 floats */
+  float* rf = g_ref_order ? (float*)calloc((size_t)256 * 119, sizeof(float)) : NULL;
+#define M3O_ACC(Jx_, w_, e_)                                                                      \
+  do {                                                                                            \
+    if (rf) {                                                                                     \
+      float* sl = rf + (size_t)(k % 256) * 119;                                                   \
+      m3o_accum_row_f(sl, sl + 105, sl + 112, Jx_, w_, e_);                                       \
+    } else {                                                                                      \
+      m3o_accum_row(hij, vi, vj, Jx_, w_, e_);                                                    \
+    }                                                                                             \
+  } while (0)
   const float sa_inv = (float)(1.0 / (double)P->sigma_a);
   const float sb_inv = P->mode == 0 ? 0.0f : (float)(1.0 / (double)P->sigma_b);
   for (int k = 0; k < N; k++) {
@@ -546,11 +581,11 @@ static void m3o_linearize_edge(const m3o_ba_params* P, const float* Twc, const f
       const float J1[7] = {0, 1, 0, -Xj_Ci[2], 0, Xj_Ci[0], Xj_Ci[1]};
       const float J2[7] = {0, 0, 1, Xj_Ci[1], -Xj_Ci[0], 0, Xj_Ci[2]};
       m3o_row(J0, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[0], err[0]);
+      M3O_ACC(Jx, w[0], err[0]);
       m3o_row(J1, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[1], err[1]);
+      M3O_ACC(Jx, w[1], err[1]);
       m3o_row(J2, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[2], err[2]);
+      M3O_ACC(Jx, w[2], err[2]);
     } else if (P->mode == 1) {
       const float norm2_i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
       const float norm1_i = sqrtf(norm2_i);
@@ -580,13 +615,13 @@ static void m3o_linearize_edge(const m3o_ba_params* P, const float* Twc, const f
       const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.0f, 0.0f};
       const float J3[7] = {rj[0], rj[1], rj[2], 0.0f, 0.0f, 0.0f, norm1_j};
       m3o_row(J0, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[0], err[0]);
+      M3O_ACC(Jx, w[0], err[0]);
       m3o_row(J1, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[1], err[1]);
+      M3O_ACC(Jx, w[1], err[1]);
       m3o_row(J2, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[2], err[2]);
+      M3O_ACC(Jx, w[2], err[2]);
       m3o_row(J3, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[3], err[3]);
+      M3O_ACC(Jx, w[3], err[3]);
     } else {
       const int u_target = (int)(ind % P->width);
       const int v_target = (int)(ind / P->width);
@@ -615,13 +650,22 @@ static void m3o_linearize_edge(const m3o_ba_params* P, const float* Twc, const f
                            fy * x_div_z * y_div_z, fy * x_div_z, 0.0f};
       const float J2[7] = {0.0f, 0.0f, zj_inv, y_div_z, -x_div_z, 0.0f, 1.0f};
       m3o_row(J0, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[0], err[0]);
+      M3O_ACC(Jx, w[0], err[0]);
       m3o_row(J1, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[1], err[1]);
+      M3O_ACC(Jx, w[1], err[1]);
       m3o_row(J2, ti, qi, si, Jx);
-      m3o_accum_row(hij, vi, vj, Jx, w[2], err[2]);
+      M3O_ACC(Jx, w[2], err[2]);
     }
     (void)Jl;
+  }
+#undef M3O_ACC
+  if (rf) {  /* the float block reductions, in the reference's order (gs first, then hij) */
+    for (int n = 0; n < 7; n++) {
+      vi[n] = (double)m3o_block_reduce(rf + 105 + n, 119);
+      vj[n] = (double)m3o_block_reduce(rf + 112 + n, 119);
+    }
+    for (int l = 0; l < 105; l++) hij[l] = (double)m3o_block_reduce(rf + l, 119);
+    free(rf);
   }
   for (int n = 0; n < 7; n++) {
     gout[n] = vi[n];

@@ -74,6 +74,7 @@ def lib():
         L.m3o_pose_retr.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int]
         L.m3o_exp_sim3.argtypes = [_f32p, _f32p]
         L.m3o_set_threads.argtypes = [ctypes.c_int]
+        L.m3o_set_ref_order.argtypes = [ctypes.c_int]
         L.m3o_act_sim3.argtypes = [_f32p, _f32p, _f32p]
         L.m3o_rel_sim3.argtypes = [_f32p, _f32p, _f32p]
         _LIB = L
@@ -142,6 +143,12 @@ def ba_params(mode, sigma_a, sigma_b=0.0, C_thresh=0.0, Q_thresh=1.5, K=None, he
         fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
     return np.array([sigma_a, sigma_b, C_thresh, Q_thresh, fx, fy, cx, cy, height, width, pixel_border, z_eps],
                     np.float32)
+
+
+def set_ref_order(on):
+    """BA sums in the reference's own fp32 order (256 per-thread float accumulators + the float blockReduce tree,
+    gn_kernels.cu:36-55) instead of per-point fp32 products summed in fp64 (the default)."""
+    lib().m3o_set_ref_order(1 if on else 0)
 
 
 def set_threads(n):
