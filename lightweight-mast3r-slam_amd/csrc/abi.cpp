@@ -796,16 +796,19 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     for (int l = 0; l <= S.nlev; l++)
       if (tasks[l] > thr) last = l;
     Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
-  } else if (flow_on && !(senv != nullptr && atoi(senv) < 0)) {
-    // subtree phase (default with the dataflow schedule): steps [0, cut) run as ONE launch, one workgroup per
-    // subtree below the cut; the rest in the one-workgroup kernel. The cut minimises the estimated finish time:
-    // the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor schedule's makespan (the
-    // back substitution does not depend on the cut), among the cuts whose schedule fits the kernel's LDS.
-    // M3S_BA_SUB=c (tests, experiments) forces the cut, -1 the launched wide steps below.
+  } else if (flow_on && senv != nullptr && atoi(senv) >= 0) {
+    // subtree phase (M3S_BA_SUB=c; an option, not the default): steps [0, cut) run as ONE launch, one workgroup
+    // per subtree below the cut; the rest in the one-workgroup kernel. c = 0 picks the cut that minimises the
+    // estimated finish time (the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor
+    // schedule's makespan), among the cuts whose schedule fits the kernel's LDS. Measured on MI355X (DESIGN.md §4
+    // BA): slower than the launched wide steps at every cut on the C5 / C4 graphs (solve 0.45-0.53 vs 0.40-0.42 ms):
+    // a subtree task's dependent global round trips cost what a launched step does, and the spine-targeted groups
+    // of the subtree steps lengthen the one-workgroup schedule.
+    const int forced = atoi(senv);
     std::vector<std::pair<double, int>> cand;
     std::vector<int> tmp_t;
     for (int cut = 0; cut < lmax; cut++) {
-      if (senv != nullptr && cut != std::max(0, std::min(atoi(senv), lmax - 1))) continue;
+      if (forced > 0 && cut != std::min(forced, lmax - 1)) continue;
       double sub_us = 0.0;
       if (cut > 0) ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &tmp_t, &sub_us);
       std::vector<int> sc;

@@ -204,11 +204,11 @@ def test_ba_k256_graph_vs_fp64_truth(request, mode, traj, solver, monkeypatch):
 def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
     """The block-sparse factorisation's schedules run the same per-task arithmetic in the same per-column order, so
     poses and dx must be bit-identical on the K=256 chess graph:
-      * the subtree phase (default; ba_subtree_kernel: one launch, one workgroup per elimination subtree below a cut,
-        the rest in one workgroup) at the plan's cost-model cut and at forced cuts (M3S_BA_SUB=c);
-      * wide elimination-tree steps as multi-workgroup launches (M3S_BA_SUB=-1: the launch-cost model's split;
+      * wide elimination-tree steps as multi-workgroup launches (default: the launch-cost model's split;
         M3S_BA_WIDE=t: every step up to the last one wider than t tasks, 0: every step, huge: all steps inside one
-        workgroup), each with the one-workgroup part on its dataflow schedule and level-synchronous (M3S_BA_FLOW=0)."""
+        workgroup), each with the one-workgroup part on its dataflow schedule and level-synchronous (M3S_BA_FLOW=0);
+      * the optional subtree phase (ba_subtree_kernel: one launch, one workgroup per elimination subtree below a cut,
+        the rest in one workgroup) at forced cuts and at its cost model's cut (M3S_BA_SUB=c, 0)."""
     import mast3r_slam_backends as B
 
     G = chess_graph
@@ -226,7 +226,7 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
         dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
         return T.cpu().numpy(), dx.cpu().numpy()
 
-    envs = [{}, {"M3S_BA_SUB": "8"}, {"M3S_BA_SUB": "24"}, {"M3S_BA_SUB": "1"}]
+    envs = [{}, {"M3S_BA_SUB": "0"}, {"M3S_BA_SUB": "8"}, {"M3S_BA_SUB": "24"}, {"M3S_BA_SUB": "1"}]
     for flow in ("1", "0"):
         envs += [{"M3S_BA_FLOW": flow, "M3S_BA_SUB": "-1"}]
         envs += [{"M3S_BA_FLOW": flow, "M3S_BA_WIDE": w} for w in ("1000000", "16", "0")]
