@@ -246,8 +246,10 @@ def bench_store(args, dev, frames=60, warmup=10):
 def roofline(kern, N, gn_iters_mean):
     """Algorithmic bytes / flops per launch / measured HIP-event duration."""
     per_px_bytes = {
-        "prep_rays": 12 + 96 + 36 + 48,  # X11 + D11 f32 in; rays9 + D11 f16 out
-        "proj_occlusion": 12 + 8 + 36 + 12 + 8 + 1,  # X21, idx_init, rays9, X11 gather, p1, valid
+        "prep_rays": 12 + 36,  # X11 in; rays9 out
+        # X21, idx_init, rays9, X11 gather, p1, valid; + the planar descriptor conversion riding along (D11 f32 in,
+        # D11 f16 out)
+        "proj_occlusion": 12 + 8 + 36 + 12 + 8 + 1 + 96 + 48,
         "refine_lin": 48 + 96 + 8 + 8,  # D11 f16 centre rows, D21 f32, p1, idx
         "track_setup": 8 + 1 + 12 + 4 + 4 + 12 + 4 + 4 + 32,  # idx, valid, Xf, Cf, Qff, Xk, Ck, Qkf -> rec
         "gn_iters": 32 * gn_iters_mean,  # 32 B record per point per iteration

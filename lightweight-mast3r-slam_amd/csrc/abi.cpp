@@ -21,13 +21,12 @@
 #include "m3s_track.h"
 
 extern "C" {
-hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, float*, int, hipStream_t);
+hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, unsigned*, hipStream_t);
 int m3s_refine_tile_ok(int, int, int, int, int, int);
-int m3s_prep_parts(int, int, int);
 hipError_t m3s_launch_iter_proj(const float*, const float*, const float*, float*, uint8_t*, int, int, int, int, int,
                                 float, float, hipStream_t);
 hipError_t m3s_launch_proj_occlusion(const float*, const float*, const float*, const int64_t*, int*, uint8_t*, int, int,
-                                     int, int, float, float, float, int*, const float*, int, float*, hipStream_t);
+                                     int, int, float, float, float, int*, const float*, void*, unsigned*, hipStream_t);
 hipError_t m3s_launch_refine_f16(const void*, const void*, const int64_t*, int64_t*, int, int, int, int, int, int, int,
                                  hipStream_t);
 hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int64_t*, int, int, int, int, int, int,
@@ -216,9 +215,7 @@ struct MatchWs {
   int* p1;        // (B,N,2) int32
   int4* olist;    // (B*N) refine deferred-outlier records
   int* ocount;    // refine deferred-outlier count
-  float* cpart;   // prep's per-block descriptor-norm maxima (the refine screen's bound)
-  float* cmax;    // their maximum (proj_occlusion reduces, refine reads)
-  int nparts;
+  unsigned* cmax;  // the refine screen's descriptor-norm bound (float bits; prep zeroes, the proj launch raises)
 };
 
 static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
@@ -227,9 +224,7 @@ static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
   w->p1 = c.take<int>((size_t)B * H * W * 2);
   w->olist = c.take<int4>((size_t)B * H * W);
   w->ocount = c.take<int>(1);
-  w->nparts = m3s_prep_parts(B, H, W);
-  w->cpart = c.take<float>((size_t)w->nparts);
-  w->cmax = c.take<float>(1);
+  w->cmax = c.take<unsigned>(1);
   return c.off;
 }
 
@@ -263,14 +258,16 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   const bool screen = (screen_env == nullptr || atoi(screen_env) != 0) && planar;
   {
     Span sp("prep_rays", s);
-    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 ? D11 : nullptr, D11h, B, H, W, F, screen ? w.cpart : nullptr,
-                            planar, s),
+    // the (B,H,W,F) f16 descriptors for the per-pixel refine kernels here; the tile path's planar ones ride along
+    // with the proj launch (off the frame's dependency chain)
+    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 && !planar ? D11 : nullptr, D11h, B, H, W, F,
+                            screen ? w.cmax : nullptr, s),
             "match prep launch");
   }
   {
     Span sp("proj_occlusion", s);
     HIP_TRY(m3s_launch_proj_occlusion(rays9, X11, X21, idx_init, p1, valid_out, B, H, W, max_iter, lambda_init,
-                                      cost_thresh, dist_thresh, w.ocount, w.cpart, w.nparts,
+                                      cost_thresh, dist_thresh, w.ocount, planar ? D11 : nullptr, D11h,
                                       screen ? w.cmax : nullptr, s),
             "match proj launch");
   }
@@ -279,7 +276,7 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   {
     Span sp("refine_lin", s);
     HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, w.olist,
-                                  w.ocount, screen ? w.cmax : nullptr, s),
+                                  w.ocount, screen ? reinterpret_cast<const float*>(w.cmax) : nullptr, s),
             "match refine launch");
   }
   return M3S_OK;

@@ -26,9 +26,8 @@ namespace m3s {
 #define PREP_T 16
 __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict__ X11, float* __restrict__ rays9,
                                                         const float* __restrict__ D11, h1* __restrict__ D11h, int H,
-                                                        int W, int F, float* __restrict__ cnorm_part, int planar) {
+                                                        int W, int F, unsigned* __restrict__ cmax_zero) {
   __shared__ float tile[(PREP_T + 2) * (PREP_T + 2) * 3];
-  __shared__ float s_ss[PREP_T * PREP_T * 8];  // per pixel, per 4-channel group: sum of squares of the f16 values
   const int b = blockIdx.z;
   const int u0 = blockIdx.x * PREP_T, v0 = blockIdx.y * PREP_T;
   const float* Xb = X11 + (size_t)b * H * W * 3;
@@ -66,8 +65,11 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
     }
 #undef T3
   }
+  if (cmax_zero != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    *cmax_zero = 0u;  // the refine screen's norm bound: +0.0f, raised by atomicMax in the proj launch
   if (D11 != nullptr) {
-    // f32 -> f16 of this tile's descriptor rows, 4 channels per lane-step
+    // f32 -> f16 of this tile's descriptor rows (B,H,W,F), 4 channels per lane-step (the per-pixel kernels'
+    // layout; the refine tile path's planar layout is written by the proj launch, desc_planar below)
     for (int t = threadIdx.x; t < PREP_T * PREP_T * (F / 4); t += blockDim.x) {
       const int pix = t / (F / 4), q = t % (F / 4);
       const int xx = u0 + pix % PREP_T, yy = v0 + pix / PREP_T;
@@ -75,47 +77,39 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
         const size_t off = (((size_t)b * H + yy) * W + xx) * F + q * 4;
         const float4 v = *reinterpret_cast<const float4*>(D11 + off);
         h1 r[4] = {(h1)v.x, (h1)v.y, (h1)v.z, (h1)v.w};
-        // planar (refine tile path, F = 24): image b's chunk plane q / 2 holds (H, W, 8)
-        const size_t hoff = planar ? ((size_t)b * 3 + (q >> 1)) * H * W * 8 + ((size_t)yy * W + xx) * 8 + (q & 1) * 4
-                                   : off;
-        *reinterpret_cast<uint2*>(D11h + hoff) = *reinterpret_cast<uint2*>(r);
-        if (cnorm_part != nullptr) {
-          const float a = (float)r[0], c = (float)r[1], d = (float)r[2], e = (float)r[3];
-          s_ss[pix * 8 + q] = a * a + c * c + d * d + e * e;
-        }
-      } else if (cnorm_part != nullptr) {
-        s_ss[pix * 8 + q] = 0.0f;
+        *reinterpret_cast<uint2*>(D11h + off) = *reinterpret_cast<uint2*>(r);
       }
-    }
-    if (cnorm_part != nullptr) {
-      // the refine screen's descriptor-norm bound (refine.hip): max over this tile's pixels of |D11h[pixel]|_2,
-      // one partial per block; proj_occlusion_kernel reduces the partials before refine reads the maximum.
-      // NaN / inf descriptors give a NaN / inf partial, which switches the screen off for every lane.
-      __syncthreads();
-      float ss = 0.0f;
-      for (int k = 0; k < F / 4; k++) ss += s_ss[threadIdx.x * 8 + k];
-      float nmax = sqrtf(ss);
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
-      __syncthreads();  // every s_ss read is done: reuse the first words for the wave maxima
-      if ((threadIdx.x & 63) == 0) s_ss[threadIdx.x >> 6] = nmax;
-      __syncthreads();
-      if (threadIdx.x == 0)
-        cnorm_part[((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
-            fmaxf_nan(fmaxf_nan(s_ss[0], s_ss[1]), fmaxf_nan(s_ss[2], s_ss[3]));
     }
   }
 }
 
-// max of the prep partials into cmax[0] (the screen's descriptor-norm bound), by the first wave of block 0 of
-// the launch that runs between prep and refine
-__device__ __forceinline__ void reduce_cnorm(const float* __restrict__ part, int nparts, float* __restrict__ cmax) {
-  const int lane = threadIdx.x & 63;
-  float m = 0.0f;
-  for (int i = lane; i < nparts; i += 64) m = fmaxf_nan(m, part[i]);
+// Refine tile path: D11 (B,H,W,24) f32 -> f16 (RNE, == torch .half()) into image b's three chunk planes (H,W,8), one
+// pixel per thread (one 16-B store per plane: lanes store consecutive pixels), and the refine screen's bound
+// max |D11h[pixel]|_2 (refine.hip) raised by one atomicMax per wave on the float's bits (non-negative: ordered as
+// unsigned; a NaN has the largest bits and wins, which switches the screen off for every lane). Run by extra blocks
+// of the proj_occlusion launch: HBM-bound conversion beside the latency-bound LM search, off the frame's chain.
+__device__ __forceinline__ void desc_planar(const float* __restrict__ D11, h1* __restrict__ D11h, int b, int n, int N,
+                                            unsigned* __restrict__ cmax) {
+  float ss = 0.0f;
+  if (n < N) {
+    const float4* src = reinterpret_cast<const float4*>(D11 + ((size_t)b * N + n) * 24);
+    const size_t plane = (size_t)N * 8;
+    h1* dst = D11h + (size_t)b * 3 * plane + (size_t)n * 8;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m = fmaxf_nan(m, __shfl_xor(m, off, 64));
-  if (lane == 0) *cmax = m;
+    for (int c = 0; c < 3; c++) {
+      const float4 v0 = src[2 * c], v1 = src[2 * c + 1];
+      h1 r[8] = {(h1)v0.x, (h1)v0.y, (h1)v0.z, (h1)v0.w, (h1)v1.x, (h1)v1.y, (h1)v1.z, (h1)v1.w};
+      *reinterpret_cast<uint4*>(dst + c * plane) = *reinterpret_cast<uint4*>(r);
+#pragma unroll
+      for (int k = 0; k < 8; k++) ss += (float)r[k] * (float)r[k];
+    }
+  }
+  if (cmax != nullptr) {
+    float nmax = sqrtf(ss);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(cmax, __float_as_uint(nmax));
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -234,11 +228,20 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
     const float* __restrict__ rays, const float* __restrict__ X11, const float* __restrict__ X21,
     const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
     int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter,
-    const float* __restrict__ cnorm_part, int cnorm_nparts, float* __restrict__ cmax) {
+    const float* __restrict__ D11, h1* __restrict__ D11h, unsigned* __restrict__ cmax) {
   const int N = H * W;
-  if (cmax != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) reduce_cnorm(cnorm_part, cnorm_nparts, cmax);
+  // with D11: odd blocks convert the descriptors (desc_planar), even blocks run the LM search
+  int bx = blockIdx.x, nbx = gridDim.x;
+  if (D11 != nullptr) {
+    if (bx & 1) {
+      desc_planar(D11, D11h, blockIdx.y, (bx >> 1) * blockDim.x + threadIdx.x, N, cmax);
+      return;
+    }
+    bx >>= 1;
+    nbx = (nbx + 1) >> 1;
+  }
   // contiguous pixel runs per XCD: each XCD's L2 then holds the rays rows its LM gathers touch
-  const int n = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int n = xcd_remap(bx, nbx) * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (zero_counter != nullptr && n == 0 && b == 0) *zero_counter = 0;  // refine's outlier list (next launch)
   if (n >= N) return;
@@ -394,18 +397,14 @@ __global__ void __launch_bounds__(256) refine_f32_kernel(const float* __restrict
 // ------------------------------------------------------------------------------------------
 // launchers (called from abi.cpp)
 // ------------------------------------------------------------------------------------------
-// cnorm_part (nullable): m3s_prep_parts(B, H, W) floats, the per-block descriptor-norm maxima (F <= 32)
-extern "C" int m3s_prep_parts(int B, int H, int W) {
-  return ((W + PREP_T - 1) / PREP_T) * ((H + PREP_T - 1) / PREP_T) * B;
-}
-
+// D11 (nullable): convert the descriptors here in the (B,H,W,F) layout (per-pixel refine kernels); the planar
+// layout of the refine tile path is converted by the proj launch instead. cmax_zero (nullable): reset the screen's
+// norm bound for this call.
 extern "C" hipError_t m3s_launch_prep(const float* X11, float* rays9, const float* D11, void* D11h, int B, int H,
-                                      int W, int F, float* cnorm_part, int planar, hipStream_t s) {
-  if (planar && F != 24) return hipErrorInvalidValue;
-  if (F > 32 || F % 4 != 0) cnorm_part = nullptr;
+                                      int W, int F, unsigned* cmax_zero, hipStream_t s) {
   dim3 grid((W + PREP_T - 1) / PREP_T, (H + PREP_T - 1) / PREP_T, B);
   hipLaunchKernelGGL(m3s::prep_rays_kernel, grid, dim3(256), 0, s, X11, rays9, D11,
-                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, D11 != nullptr ? cnorm_part : nullptr, planar);
+                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, cmax_zero);
   return hipGetLastError();
 }
 
@@ -421,11 +420,13 @@ extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, 
 extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* X11, const float* X21,
                                                 const int64_t* idx_init, int* p1, uint8_t* valid, int B, int H, int W,
                                                 int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-                                                int* zero_counter, const float* cnorm_part, int cnorm_nparts,
-                                                float* cmax, hipStream_t s) {
-  dim3 grid((H * W + 255) / 256, B);
+                                                int* zero_counter, const float* D11, void* D11h, unsigned* cmax,
+                                                hipStream_t s) {
+  // D11 (nullable, F = 24): the planar conversion for the refine tile path rides along (odd blocks; desc_planar)
+  dim3 grid((H * W + 255) / 256 * (D11 != nullptr ? 2 : 1), B);
   hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
-                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter, cnorm_part, cnorm_nparts, cmax);
+                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter, D11,
+                     reinterpret_cast<m3s::h1*>(D11h), cmax);
   return hipGetLastError();
 }
 

@@ -146,6 +146,20 @@ __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, fl
   }
 }
 
+// bit c set where a[c] >= T (c < 49; NaN never), two VALU per candidate: the compare's lane bit shifted into the mask
+// word by an add-with-carry (m = m + m + vcc), candidates in descending order so candidate c lands on bit c. The
+// compiler's select / or / 64-bit shift form took about four per candidate.
+__device__ __forceinline__ uint64_t screen_mask(const float* a, float T) {
+  unsigned lo = 0u, hi = 0u;
+#pragma unroll
+  for (int c = 48; c >= 32; c--)
+    asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(hi) : "v"(a[c]), "v"(T) : "vcc");
+#pragma unroll
+  for (int c = 31; c >= 0; c--)
+    asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(lo) : "v"(a[c]), "v"(T) : "vcc");
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // exact c10::Half chains of the survivor mask m in ascending scan order, read from D11h (L2); strict '>'. Two
 // survivors per trip: both candidates' loads are in flight before the first chain (one L2 round trip per pair)
 template <int D, bool PLANAR>
@@ -326,9 +340,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #pragma unroll
       for (int c = 0; c < G * G; c++) lmax = fmaxf(lmax, ((vm >> c) & 1ull) ? a[c] : -INFINITY);
       const float T = fmaxf((float)max_score - t.bq, lmax - 2.0f * t.bq);
-      uint64_t m = 0;
-#pragma unroll
-      for (int c = 0; c < G * G; c++) m |= (a[c] >= T) ? (1ull << c) : 0ull;
+      uint64_t m = screen_mask(a, T);
       if (!t.sok) m = ~0ull;
       m &= vm;
       if (!first) m &= ~(1ull << (G * G / 2));
