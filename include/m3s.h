@@ -141,6 +141,10 @@ int m3s_ba_make_plan_kf_reuse(const m3s_ba_config* cfg, float* Twc, const m3s_ba
 /* packed_edges: shard edges the plan's pack wrote; changed_keyframes: keyframes found changed (all without reuse) */
 int m3s_ba_reuse_info(const m3s_ba_plan* plan, int* packed_edges, int* changed_keyframes);
 int m3s_ba_reuse_release(const void* workspace);
+/* The library keeps per-workspace host state for BA plans (the symbolic analysis a plan's solves use). Call
+ * m3s_ba_plan_release(workspace) once no plan on `workspace` will be solved again and before freeing or repurposing
+ * it (m3s_ba_reuse_release does it too); it joins a pending analysis and frees its tables. */
+int m3s_ba_plan_release(const void* workspace);
 int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count);
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);
@@ -243,7 +247,12 @@ typedef struct m3s_track_result {
   int iters, status, n_valid_opt, n_valid_kf, n_unique, N;
 } m3s_track_result;
 
+/* The track workspace's frame scratch (byte map, counters, tickets) persists across calls: each call's fusion launch
+ * leaves it clean for the next frame, so only a fresh workspace is initialised. Call m3s_track_release(workspace)
+ * before freeing or repurposing a workspace m3s_track used (a later workspace at the same address is then
+ * initialised again); a workspace of another size at the same address is always initialised. */
 size_t m3s_track_workspace_size(int N);
+int m3s_track_release(const void* workspace);
 int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg, const m3s_track_fuse_args* fuse,
               int first_chunk, float* T_out_dev /* (16) nullable: T_WCf | T_CkCf on device */,
               m3s_track_result* result /* host */, void* workspace, size_t workspace_bytes, void* stream);

@@ -317,9 +317,16 @@ static int wait_published(const TrackMirror* m, unsigned gen, hipStream_t s) {
   }
 }
 
-// workspaces whose frame scratch the last fuse launch cleared: workspace -> clean byte-map entries (uint4)
+// workspaces whose frame scratch the last fuse launch cleared: workspace -> {clean byte-map entries (uint4), the
+// workspace's size}; an entry is dropped by m3s_track_release (the caller frees or repurposes the workspace)
 static std::mutex g_track_clean_mu;
-static std::map<const void*, int> g_track_clean;
+static std::map<const void*, std::pair<int, size_t>> g_track_clean;
+
+extern "C" int m3s_track_release(const void* workspace) {
+  std::lock_guard<std::mutex> lock(g_track_clean_mu);
+  g_track_clean.erase(workspace);
+  return M3S_OK;
+}
 
 static int track_nparts(int N) { return std::max(1, std::min(256, (N + 1023) / 1024)); }  // <= 1 block per CU
 
@@ -439,7 +446,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   {
     std::lock_guard<std::mutex> lock(g_track_clean_mu);
     auto it = g_track_clean.find(workspace);
-    if (it != g_track_clean.end()) clean = it->second;
+    if (it != g_track_clean.end() && it->second.second == workspace_bytes) clean = it->second.first;
     g_track_clean.erase(workspace);  // dirty until this call has published
   }
   if (clean < n16) {
@@ -468,7 +475,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   if (int rc = wait_published(mirror, pub.gen, s)) return rc;
   {
     std::lock_guard<std::mutex> lock(g_track_clean_mu);
-    g_track_clean[workspace] = clean;  // the fuse launch cleared what this frame dirtied
+    g_track_clean[workspace] = {clean, workspace_bytes};  // the fuse launch cleared what this frame dirtied
   }
   const TrackState& hs = mirror->s;
   if (hs.status == M3S_TRACK_STALLED)
@@ -1301,7 +1308,21 @@ extern "C" int m3s_ba_reuse_info(const m3s_ba_plan* plan, int* packed_edges, int
   return M3S_OK;
 }
 
+extern "C" int m3s_ba_plan_release(const void* workspace) {
+  std::unique_ptr<PlanSym> Y;
+  {
+    std::lock_guard<std::mutex> lock(g_sym_mu);
+    auto it = g_sym.find(workspace);
+    if (it == g_sym.end()) return M3S_OK;
+    Y = std::move(it->second);
+    g_sym.erase(it);
+  }
+  if (Y && !Y->joined && Y->fut.valid()) Y->fut.wait();  // the worker writes into Y: done before it is freed
+  return M3S_OK;
+}
+
 extern "C" int m3s_ba_reuse_release(const void* workspace) {
+  m3s_ba_plan_release(workspace);
   std::lock_guard<std::mutex> lock(g_rec_mu);
   auto it = g_rec.find(workspace);
   if (it == g_rec.end()) return M3S_OK;

@@ -94,6 +94,7 @@ _SIGS = {
                                    c_void_p], c_int),
     "m3s_ba_reuse_info": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), ctypes.POINTER(c_int)], c_int),
     "m3s_ba_reuse_release": ([c_void_p], c_int),
+    "m3s_ba_plan_release": ([c_void_p], c_int),
     "m3s_ba_edge_sums": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)], c_int),
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
@@ -104,6 +105,7 @@ _SIGS = {
     "m3s_match_workspace_size": ([c_int] * 4, c_size_t),
     "m3s_match": ([c_void_p] * 7 + [c_int] * 5 + [c_float] * 3 + [c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
     "m3s_track_workspace_size": ([c_int], c_size_t),
+    "m3s_track_release": ([c_void_p], c_int),
     "m3s_codebook_size": ([c_int, c_int], c_size_t),
     "m3s_codebook_prepare": ([c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p], c_int),
     "m3s_quantize_workspace_size": ([c_int] * 4, c_size_t),
@@ -179,6 +181,9 @@ def ptr(t):
 _WS = {}
 
 
+_WS_RELEASE = {"track": "m3s_track_release", "ba": "m3s_ba_plan_release"}  # key -> the ABI call that forgets a dropped buffer
+
+
 def workspace(key, nbytes, device, stream):
     """A cached uint8 device buffer per (key, device, stream), grown on demand (torch caching allocator).
 
@@ -187,6 +192,10 @@ def workspace(key, nbytes, device, stream):
     k = (key, device, stream.value)
     buf = _WS.get(k)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None and key in _WS_RELEASE and _LIB is not None:
+            # the library's per-workspace state of the buffer being dropped (m3s_track_release: its "clean
+            # scratch" record; the allocator may hand the same address to another buffer later)
+            getattr(_LIB, _WS_RELEASE[key])(buf.data_ptr())
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _WS[k] = buf
     return buf

@@ -114,6 +114,7 @@ class HipShard:
             ru = ctypes.byref(_lib.BaReuse(edge_uid.ctypes.data, kf_uid.ctypes.data))
         else:
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            self._own_ws = True
             ru = None
         self.keep = (Twc, Xs, Cs, ii, jj, idx, valid, Q, keyframes)
         self.plan = _lib.BaPlan()
@@ -133,6 +134,14 @@ class HipShard:
         off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
         _lib.check(lib.m3s_ba_edge_sums(ctypes.byref(self.plan), ctypes.byref(off), ctypes.byref(cnt)))
         self.edge_sums = self.ws[off.value: off.value + cnt.value].view(torch.float64)
+
+    def __del__(self):
+        # a workspace of its own (not the RecordCache's): the library's plan state for it goes with it
+        try:
+            if getattr(self, "_own_ws", False) and _lib._LIB is not None:
+                _lib._LIB.m3s_ba_plan_release(_lib.ptr(self.ws))
+        except Exception:  # interpreter shutdown
+            pass
 
     def reuse_info(self):
         """(shard edges the pack wrote, keyframes found changed)."""

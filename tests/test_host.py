@@ -295,3 +295,18 @@ def test_factor_graph_rejects_pin_other_than_one():
         for fn in (fg.solve_GN_rays, fg.solve_GN_calib):
             with pytest.raises(ValueError, match="pin"):
                 fn()
+
+
+def test_workspace_release_entry_points_are_safe_without_state():
+    """m3s_track_release / m3s_ba_plan_release / m3s_ba_reuse_release forget the library's per-workspace host state
+    (a freed workspace's address can be reused): they succeed on an address the library never saw and
+    need no GPU."""
+    from m3s import _lib
+
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in ("m3s_track_release", "m3s_ba_plan_release", "m3s_ba_reuse_release"):
+        fn = getattr(lib, name)
+        fn.argtypes = [ctypes.c_void_p]
+        fn.restype = ctypes.c_int
+        assert fn(ctypes.c_void_p(0x1234000)) == 0
+        assert fn(None) == 0
