@@ -38,7 +38,7 @@ hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int
 hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, const TrackPublish*, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 int m3s_track_max_parts(void);
-hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, hipStream_t);
+hipError_t m3s_launch_ba_lin(const BaArgs*, const BaParams*, int, int, hipStream_t);
 hipError_t m3s_launch_ba_pack(const BaArgs*, const BaParams*, int, hipStream_t);
 hipError_t m3s_launch_ba_kf_compare(const BaKfCopy*, int, int, uint8_t*, hipStream_t);
 hipError_t m3s_launch_ba_solve(const BaArgs*, int, int, float, const int*, const int*, const int*, hipStream_t);
@@ -704,6 +704,7 @@ struct PlanSym {
   size_t off[BA_SYM_SECTIONS] = {0};
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
   int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
+  bool pack_deferred = false;    // the plan's pack runs inside its first linearisation (set at plan time, under g_sym_mu)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
   int step_na[BA_MAX_WIDE_STEPS] = {0};    // its factor tasks (update groups follow)
@@ -1234,7 +1235,15 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.n_packed = RC ? (int)pack.size() : EL;
   P.n_dirty = 0;
   for (int k = 0; k < Kp; k++) P.n_dirty += kdirty[k];
-  {
+  // every shard edge packs (no reuse, or a first reuse plan): the pack's gathers run inside the first
+  // linearisation (ba_lin_kernel<PACK>: HBM-bound gathers under VALU-bound rows, one launch fewer);
+  // M3S_BA_FUSED_PACK=0 keeps the separate pack launch (A/B)
+  const char* fpe = getenv("M3S_BA_FUSED_PACK");
+  const bool defer = P.n_packed == EL && EL > 0 && !(fpe && !strcmp(fpe, "0"));
+  if (defer) {
+    std::lock_guard<std::mutex> lock(g_sym_mu);
+    Y->pack_deferred = true;
+  } else {
     Span sp("ba_pack", s);
     HIP_TRY(m3s_launch_ba_pack(&P.a, &P.p, P.n_packed, s), "ba pack launch");
   }
@@ -1365,8 +1374,17 @@ extern "C" int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream) {
   // a shard writes only its own rows: clear the rest so the caller's all-reduce sums fresh rows
   if ((P->e0 > 0 || P->e1 < P->E) && P->edge_sums_bytes > 0)
     HIP_TRY(hipMemsetAsync(P->a.edge_sums, 0, P->edge_sums_bytes, s), "ba memset");
-  Span sp("ba_linearize", s);
-  HIP_TRY(m3s_launch_ba_lin(&P->a, &P->p, P->e1 - P->e0, s), "ba linearize launch");
+  int pack = 0;  // this plan's first linearisation also packs (see ba_make_plan_impl)
+  {
+    std::lock_guard<std::mutex> lock(g_sym_mu);
+    auto it = g_sym.find(P->ws);
+    if (it != g_sym.end() && it->second->gen == P->sym_gen && it->second->pack_deferred) {
+      pack = 1;
+      it->second->pack_deferred = false;
+    }
+  }
+  Span sp(pack ? "ba_lin_pack" : "ba_linearize", s);
+  HIP_TRY(m3s_launch_ba_lin(&P->a, &P->p, P->e1 - P->e0, pack, s), "ba linearize launch");
   return M3S_OK;
 }
 

@@ -173,6 +173,28 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
 // Only the edges of a.pack_list when the plan reuses records (m3s_ba_make_plan_reuse: the rest kept theirs), each
 // into its record slot.
+// the record of point k of shard edge e (ix, jx: its pose ranks)
+template <int MODE>
+__device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k) {
+  const int N = p.N;
+  const size_t g = (size_t)(e + p.edge_offset) * N + k;
+  const bool vm = a.valid[g] != 0;
+  const int64_t ind = vm ? a.idx[g] : 0;
+  const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
+  const float q = a.Q[g];
+  const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
+                     (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
+  // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
+  const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
+  if constexpr (MODE == BA_MODE_CALIB) {
+    const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
+    const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
+    return make_float4((float)u_t, (float)v_t, Xi[2], sw);
+  } else {
+    return make_float4(Xi[0], Xi[1], Xi[2], sw);
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack) {
   const int N = p.N;
@@ -180,25 +202,7 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
     const int t = (int)(o / N), k = (int)(o - (size_t)t * N);
     const int e = a.pack_list ? a.pack_list[t] : t;
-    const size_t g = (size_t)(e + p.edge_offset) * N + k;
-    const int ix = a.ii_rank[e], jx = a.jj_rank[e];
-    const bool vm = a.valid[g] != 0;
-    const int64_t ind = vm ? a.idx[g] : 0;
-    const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
-    const float q = a.Q[g];
-    const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
-                       (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
-    // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
-    const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
-    float4 r;
-    if constexpr (MODE == BA_MODE_CALIB) {
-      const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
-      const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
-      r = make_float4((float)u_t, (float)v_t, Xi[2], sw);
-    } else {
-      r = make_float4(Xi[0], Xi[1], Xi[2], sw);
-    }
-    a.rec[(size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k] = r;
+    a.rec[(size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k);
   }
 }
 
@@ -238,7 +242,10 @@ __global__ void __launch_bounds__(256) ba_kf_compare_kernel(const BaKfCopy* __re
   if (__any(diff) && (threadIdx.x & 63) == 0) dirty[k] = 1;
 }
 
-template <int MODE>  // specialised per residual type: one mode's registers, not the union of three
+// PACK: the first GN iteration of a call that packs every edge builds each point's record itself (pack_record, the
+// same values) and stores it for the later iterations: the pack's gathers (HBM-bound) run under this kernel's
+// VALU-bound rows instead of as a separate launch before it.
+template <int MODE, bool PACK>  // specialised per residual type: one mode's registers, not the union of three
 __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaParams p) {
   if (*a.done) return;
   // the plan's block table: edges grouped by target keyframe, consecutive blocks on one XCD (xcd_remap)
@@ -287,7 +294,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
 #endif
-  const float4* rec = a.rec + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;
+  float4* rec = a.rec + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;
   const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
@@ -310,7 +317,16 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     // a missing second point repeats the first with weight 0: it adds exact zeros unless the first point's own
     // row is non-finite, which poisons the sums anyway (another point as filler changed the rays sums)
     const int k1c = has1 ? k1 : k0;
-    const float4 R0 = rec[k0], R1 = rec[k1c];
+    float4 R0, R1;
+    if constexpr (PACK) {
+      R0 = pack_record<MODE>(a, p, e, ix, jx, k0);
+      R1 = has1 ? pack_record<MODE>(a, p, e, ix, jx, k1) : R0;
+      rec[k0] = R0;
+      if (has1) rec[k1] = R1;
+    } else {
+      R0 = rec[k0];
+      R1 = rec[k1c];
+    }
     f2 Xj[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) Xj[c] = f2{Xj_base[(size_t)k0 * 3 + c], Xj_base[(size_t)k1c * 3 + c]};
@@ -1270,15 +1286,24 @@ extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int
   return hipGetLastError();
 }
 
-extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int E_local, hipStream_t s) {
+// pack (first iteration of a call whose pack was deferred): the linearisation also builds and stores the records
+extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int E_local, int pack, hipStream_t s) {
   if (E_local <= 0) return hipSuccess;
   const dim3 g(E_local * p->chunks);
+#define BA_LIN_LAUNCH(M)                                                                        \
+  do {                                                                                          \
+    if (pack)                                                                                   \
+      hipLaunchKernelGGL((m3s::ba_lin_kernel<M, true>), g, dim3(256), 0, s, *a, *p);              \
+    else                                                                                        \
+      hipLaunchKernelGGL((m3s::ba_lin_kernel<M, false>), g, dim3(256), 0, s, *a, *p);             \
+  } while (0)
   if (p->mode == BA_MODE_POINTS)
-    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p);
+    BA_LIN_LAUNCH(BA_MODE_POINTS);
   else if (p->mode == BA_MODE_RAYS)
-    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p);
+    BA_LIN_LAUNCH(BA_MODE_RAYS);
   else
-    hipLaunchKernelGGL(m3s::ba_lin_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p);
+    BA_LIN_LAUNCH(BA_MODE_CALIB);
+#undef BA_LIN_LAUNCH
   hipLaunchKernelGGL(m3s::ba_edge_kernel, dim3(E_local), dim3(64), 0, s, *a, *p, E_local);
   return hipGetLastError();
 }

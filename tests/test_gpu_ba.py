@@ -381,3 +381,23 @@ def test_factor_schedule_stall_raises_not_silent(monkeypatch):
     sh.linearize()
     sh.solve()
     assert sh.iterations() == 1 and not torch.equal(T1, G["Twc0"].to(dev))
+
+
+@pytest.mark.parametrize("mode", ["points", "rays", "calib"])
+def test_pack_fused_into_first_linearisation_is_bit_identical(mode, monkeypatch):
+    """A call that packs every edge builds the point records inside its first linearisation (ba_lin_kernel<PACK>,
+    the same pack_record values) instead of a separate ba_pack launch: poses and dx bit-identical to the separate
+    pack (M3S_BA_FUSED_PACK=0), on a 24-keyframe graph with ragged chunks."""
+    from m3s.synthetic import make_graph, two_way
+
+    G = make_graph(n_kf=24, H=48, W=66, seed=8)
+    ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
+    K = G["K"].numpy()
+    Xs = G["Xs"].numpy()
+    if mode == "calib":
+        Xs = O.backproject_constrain(Xs, K, (48, 66))
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("M3S_BA_FUSED_PACK", fused)
+        out.append(_call(mode, G["Twc0"].numpy(), Xs, G["Cs"].numpy(), ii, jj, idx, valid, Q, K, 48, 66))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
