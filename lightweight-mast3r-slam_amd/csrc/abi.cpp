@@ -613,7 +613,7 @@ PlanStage& plan_stage() {
 struct RecCache {
   bool valid = false;
   int N = 0, mode = -1, W = 0;
-  float Q_thresh = 0.0f, C_thresh = 0.0f;
+  float Q_thresh = 0.0f, C_thresh = 0.0f, z_eps = 0.0f;
   std::unordered_map<int64_t, int> slot_of;  // edge uid -> record slot (shard-local)
   std::unordered_map<int64_t, int> copy_of;  // keyframe uid -> copy index
   std::vector<uint32_t> scale;               // per copy: bits of the Cscale its records were packed with
@@ -994,7 +994,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   }
   if (RC) {
     const bool same = RC->valid && RC->N == N && RC->mode == cfg->mode && RC->Q_thresh == cfg->Q_thresh &&
-                      RC->C_thresh == cfg->C_thresh && (cfg->mode != 2 || RC->W == cfg->width);
+                      RC->C_thresh == cfg->C_thresh &&
+                      (cfg->mode != 2 || (RC->W == cfg->width && RC->z_eps == cfg->z_eps));
     if (!same) {
       RC->reset_maps();
       RC->N = N;
@@ -1002,6 +1003,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
       RC->Q_thresh = cfg->Q_thresh;
       RC->C_thresh = cfg->C_thresh;
       RC->W = cfg->width;
+      RC->z_eps = cfg->z_eps;  // calib records hold log z_i, or NaN where z_i <= z_eps
     }
     RC->valid = false;  // until this plan is complete
     std::vector<int> ci(Kp, -1);

@@ -167,7 +167,8 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 }
 
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
-//   rec[e][k] = {Xi (points / rays) or (u_t, v_t, z_i) (calib) ; sw} with Xi = Xs[i][valid ? idx : 0]
+//   rec[e][k] = {Xi (points / rays) or (u_t, v_t, log z_i | NaN if z_i <= z_eps) (calib) ; sw} with
+//   Xi = Xs[i][valid ? idx : 0]
 //   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
 //   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
@@ -189,7 +190,9 @@ __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p
   if constexpr (MODE == BA_MODE_CALIB) {
     const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
     const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
-    return make_float4((float)u_t, (float)v_t, Xi[2], sw);
+    // log z_i once per call (the same __logf the linearisation applied every iteration), NaN marks z_i <= z_eps
+    const float zi = Xi[2];
+    return make_float4((float)u_t, (float)v_t, zi > p.z_eps ? __logf(zi) : __builtin_nanf(""), sw);
   } else {
     return make_float4(Xi[0], Xi[1], Xi[2], sw);
   }
@@ -388,12 +391,12 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b0011111>(fL, fv, J2, huber_ba2(swr * err[2]) * wr, err[2]);  // {0,1,2,3,4}
       acc_local_f2<0b1000111>(fL, fv, J3, huber_ba2(swd * err[3]) * wd, err[3]);  // {0,1,2,6}
     } else {  // calib
-      const f2 u_t = Rx, v_t = Ry, zi = Rz;
-      const auto valid_z = (Y[2] > p.z_eps) & (zi > p.z_eps);
+      const f2 u_t = Rx, v_t = Ry, lzi = Rz;  // lzi: log z_i, NaN where z_i <= z_eps (pack_record)
+      const auto valid_z = (Y[2] > p.z_eps) & (lzi == lzi);
       const f2 z2 = {0.0f, 0.0f};
       const f2 zj_inv = valid_z ? f2{__builtin_amdgcn_rcpf(Y[2].x), __builtin_amdgcn_rcpf(Y[2].y)} : z2;
       const f2 zj_log = valid_z ? f2{__logf(Y[2].x), __logf(Y[2].y)} : z2;
-      const f2 zi_log = valid_z ? f2{__logf(zi.x), __logf(zi.y)} : z2;
+      const f2 zi_log = valid_z ? lzi : z2;
       const f2 xz = Y[0] * zj_inv, yz = Y[1] * zj_inv;
       const f2 u = BA_FMA2(f2{p.fx, p.fx}, xz, f2{p.cx, p.cx}), vv = BA_FMA2(f2{p.fy, p.fy}, yz, f2{p.cy, p.cy});
       const float ub = (float)p.pixel_border, uh = (float)(p.W - 1 - p.pixel_border),
