@@ -377,14 +377,15 @@ def bench_ba(args, rank, world, dev, leg):
     # roofline of the dominant kernel (the linearisation) at the build's compulsory bytes per iteration
     lin_s = spans["ba_linearize"] * 1e-3
     n_e = e1 - e0
-    alg = n_e * N * BA_REC_BYTES + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
+    rec_bytes = BA_REC_BYTES + (4 if mode == "rays" else 0)  # rays: + |Xi| (the record holds the unit ray)
+    alg = n_e * N * rec_bytes + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
     pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}>", pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     traffic = pmc["traffic_bytes"] if pmc else None
     roof = {"kernel": "ba_lin_kernel + ba_edge_kernel", "bound": "hbm", "achieved": alg / lin_s / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / lin_s / 1e9 / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_over_alg": (traffic / alg) if traffic else None,
             "traffic_source": pmc["file"] if pmc else None, "avg_us": spans["ba_linearize"] * 1e3,
-            "alg_bytes": f"{BA_REC_BYTES} B record x {N} points x {n_e} edges + {BA_XJ_BYTES} B X_j x {N} points x "
+            "alg_bytes": f"{rec_bytes} B record x {N} points x {n_e} edges + {BA_XJ_BYTES} B X_j x {N} points x "
                          f"{info['targets']} target keyframes + {2 * info['chunks'] + 1} x {BA_SUM_BYTES} B partial/"
                          f"edge-sum rows x {n_e} edges per launch (compulsory traffic, DESIGN.md §4)"}
     # the backend's next solve (main.py:150-155) on the same graph after tracking re-fused the newest keyframe, with
@@ -430,7 +431,7 @@ def bench_ba(args, rank, world, dev, leg):
     # the pack's cost: its own launch, or what it adds to the first linearisation when fused into it
     ms_pack = spans["ba_lin_pack"] - spans["ba_linearize"] if fused else spans["ba_pack"]
     pack_s = (spans["ba_lin_pack"] if fused else spans["ba_pack"]) * 1e-3
-    pack_bytes = n_e * N * BA_PACK_EDGE_BYTES + args.ba_kf * N * BA_PACK_KF_BYTES
+    pack_bytes = n_e * N * (BA_PACK_EDGE_BYTES + (4 if mode == "rays" else 0)) + args.ba_kf * N * BA_PACK_KF_BYTES
     pack_pmc = pmc_entry(f"ba_pack_kernel<{1 if mode == 'rays' else 2}>",
                          pattern=f"r[0-9][0-9]_ba{'_c4' if leg == 'C4' else ''}_pmc.json")
     out = {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,

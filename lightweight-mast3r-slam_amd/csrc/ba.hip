@@ -174,9 +174,11 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 //   gathers, int64 index loads and threshold tests leave the linearisation loop.
 // Only the edges of a.pack_list when the plan reuses records (m3s_ba_make_plan_reuse: the rest kept theirs), each
 // into its record slot.
-// the record of point k of shard edge e (ix, jx: its pose ranks)
+// the record of point k of shard edge e (ix, jx: its pose ranks); rays: *n = |Xi| (the record holds Xi / |Xi|,
+// computed with the linearisation's own instruction sequence, so the rows are bit-identical to normalising there)
 template <int MODE>
-__device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k) {
+__device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k,
+                                              float* n) {
   const int N = p.N;
   const size_t g = (size_t)(e + p.edge_offset) * N + k;
   const bool vm = a.valid[g] != 0;
@@ -193,6 +195,12 @@ __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p
     // log z_i once per call (the same __logf the linearisation applied every iteration), NaN marks z_i <= z_eps
     const float zi = Xi[2];
     return make_float4((float)u_t, (float)v_t, zi > p.z_eps ? __logf(zi) : __builtin_nanf(""), sw);
+  } else if constexpr (MODE == BA_MODE_RAYS) {
+    const f2 X[3] = {f2{Xi[0], Xi[0]}, f2{Xi[1], Xi[1]}, f2{Xi[2], Xi[2]}};
+    const f2 n2 = X[0] * X[0] + X[1] * X[1] + X[2] * X[2];
+    const f2 inv = rsq2(n2);
+    *n = (n2 * inv).x;
+    return make_float4((inv * X[0]).x, (inv * X[1]).x, (inv * X[2]).x, sw);
   } else {
     return make_float4(Xi[0], Xi[1], Xi[2], sw);
   }
@@ -205,7 +213,10 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
     const int t = (int)(o / N), k = (int)(o - (size_t)t * N);
     const int e = a.pack_list ? a.pack_list[t] : t;
-    a.rec[(size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k);
+    const size_t r = (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k;
+    float n = 0.0f;
+    a.rec[r] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n);
+    if constexpr (MODE == BA_MODE_RAYS) a.rec_n[r] = n;
   }
 }
 
@@ -298,6 +309,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
   for (int c = 0; c < 7; c++) v[c] = 0.0;
 #endif
   float4* rec = a.rec + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;
+  float* rec_n = a.rec_n + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;  // rays: |Xi|
   const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;
@@ -321,14 +333,22 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     // row is non-finite, which poisons the sums anyway (another point as filler changed the rays sums)
     const int k1c = has1 ? k1 : k0;
     float4 R0, R1;
+    f2 nI = {0.0f, 0.0f};  // rays: |Xi| of both points
     if constexpr (PACK) {
-      R0 = pack_record<MODE>(a, p, e, ix, jx, k0);
-      R1 = has1 ? pack_record<MODE>(a, p, e, ix, jx, k1) : R0;
+      R0 = pack_record<MODE>(a, p, e, ix, jx, k0, &nI.x);
+      nI.y = nI.x;
+      if (has1) R1 = pack_record<MODE>(a, p, e, ix, jx, k1, &nI.y);
+      else R1 = R0;
       rec[k0] = R0;
       if (has1) rec[k1] = R1;
+      if constexpr (MODE == BA_MODE_RAYS) {
+        rec_n[k0] = nI.x;
+        if (has1) rec_n[k1] = nI.y;
+      }
     } else {
       R0 = rec[k0];
       R1 = rec[k1c];
+      if constexpr (MODE == BA_MODE_RAYS) nI = f2{rec_n[k0], rec_n[k1c]};
     }
     f2 Xj[3];
 #pragma unroll
@@ -363,14 +383,13 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b1101010>(fL, fv, J1, huber_ba2(sw * err[1]) * wc, err[1]);  // {1,3,5,6}
       acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(sw * err[2]) * wc, err[2]);  // {2,3,4,6}
     } else if constexpr (MODE == BA_MODE_RAYS) {
-      const f2 n2i = Rx * Rx + Ry * Ry + Rz * Rz;
-      const f2 n1i_inv = rsq2(n2i);
-      const f2 n1i = n2i * n1i_inv;
+      // the record holds ri = Xi / |Xi| and rec_n |Xi| (pack_record: the same operations, once per call)
+      const f2 n1i = nI;
       const f2 n2j = Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2];
       const f2 n1j_inv = rsq2(n2j);
       const f2 n1j = n2j * n1j_inv;
       const f2 rj[3] = {n1j_inv * Y[0], n1j_inv * Y[1], n1j_inv * Y[2]};
-      const f2 err[4] = {rj[0] - n1i_inv * Rx, rj[1] - n1i_inv * Ry, rj[2] - n1i_inv * Rz, n1j - n1i};
+      const f2 err[4] = {rj[0] - Rx, rj[1] - Ry, rj[2] - Rz, n1j - n1i};
       const f2 swr = p.inv_a * sqq;
       const f2 swd = p.inv_b * sqq;
       const f2 wr = swr * swr, wd = swd * swd;

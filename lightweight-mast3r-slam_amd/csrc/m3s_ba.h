@@ -41,7 +41,8 @@ struct BaArgs {
   const int64_t* idx;    // (E,N) global edge rows
   const uint8_t* valid;  // (E,N)
   const float* Q;        // (E,N)
-  float4* rec;           // (slots, N) point records (ba_pack): {Xi | u_t, v_t, z_i ; sqrt-weight}
+  float4* rec;           // (slots, N) point records (ba_pack): {Xi | Xi/|Xi| (rays) | u_t, v_t, log z_i ; sqrt-weight}
+  float* rec_n;          // (slots, N) rays mode: |Xi| (the record holds the unit ray)
   const int* rec_slot;   // (E_local) record slot of each shard edge (record reuse across plans), or null: slot = edge
   const int* pack_list;  // (n_pack) shard edges the pack writes (the others kept their records), or null: all
   double* partials;      // (E_local*chunks, 36)
