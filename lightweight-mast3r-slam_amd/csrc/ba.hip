@@ -335,10 +335,12 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     float4 R0, R1;
     f2 nI = {0.0f, 0.0f};  // rays: |Xi| of both points
     if constexpr (PACK) {
-      R0 = pack_record<MODE>(a, p, e, ix, jx, k0, &nI.x);
-      nI.y = nI.x;
-      if (has1) R1 = pack_record<MODE>(a, p, e, ix, jx, k1, &nI.y);
+      float n0 = 0.0f, n1 = 0.0f;
+      R0 = pack_record<MODE>(a, p, e, ix, jx, k0, &n0);
+      n1 = n0;
+      if (has1) R1 = pack_record<MODE>(a, p, e, ix, jx, k1, &n1);
       else R1 = R0;
+      nI = f2{n0, n1};
       rec[k0] = R0;
       if (has1) rec[k1] = R1;
       if constexpr (MODE == BA_MODE_RAYS) {
