@@ -82,7 +82,8 @@ if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the la
           f"pull groups {st[5]}: prologue {t[1]:.1f} us, factor {t[2 + nlev] - t[1]:.1f} us, "
           f"back {t[3 + 2 * nlev] - t[2 + nlev]:.1f} us, tail {t[4 + 2 * nlev] - t[3 + 2 * nlev]:.1f} us, "
           f"total {t[4 + 2 * nlev]:.1f}")
-    print("steps:", " ".join(f"{x:.2f}" for x in steps))
+    if all(buf[2 + l] != 0 for l in range(nlev)):  # level stamps exist only in the level-synchronous build
+        print("steps:", " ".join(f"{x:.2f}" for x in steps))
     # back substitution: stamps only after barriers (runs of single-column levels share one), root level first
     bs = [(buf[3 + nlev + (nlev - 1 - l)] - buf[0]) / 100.0 for l in range(nlev - 1, -1, -1)]
     prev, segs = t[2 + nlev], []
