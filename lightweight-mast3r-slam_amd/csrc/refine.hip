@@ -146,17 +146,27 @@ __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, fl
   }
 }
 
-// bit c set where a[c] >= T (c < 49; NaN never), two VALU per candidate: the compare's lane bit shifted into the mask
-// word by an add-with-carry (m = m + m + vcc), candidates in descending order so candidate c lands on bit c. The
-// compiler's select / or / 64-bit shift form took about four per candidate.
+// bit c set where a[c] >= T (c < 49; NaN never), two VALU per candidate: the compare's lane mask (an SGPR pair) shifted
+// into the mask word by an add-with-carry (m = m + m + carry), candidates in descending order so candidate c lands on
+// bit c. The compiler's select / or / 64-bit shift form took about four per candidate. Each instruction is its own asm
+// statement and the compares run two candidates ahead of the adds: gfx950 needs two wait states between a VALU write
+// of an SGPR and a VALU read of it (the compiler pads v_cmp -> v_cndmask with s_nop 1), and the interleave provides
+// them without nops; the compiler sees every operand, so it pads wherever the distance is short (the last two adds).
 __device__ __forceinline__ uint64_t screen_mask(const float* a, float T) {
+  constexpr int C = 49;
   unsigned lo = 0u, hi = 0u;
+  unsigned long long s[C];
 #pragma unroll
-  for (int c = 48; c >= 32; c--)
-    asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(hi) : "v"(a[c]), "v"(T) : "vcc");
-#pragma unroll
-  for (int c = 31; c >= 0; c--)
-    asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(lo) : "v"(a[c]), "v"(T) : "vcc");
+  for (int k = 0; k < C + 2; k++) {
+    if (k < C) asm volatile("v_cmp_ge_f32_e64 %0, %1, %2" : "=s"(s[k]) : "v"(a[C - 1 - k]), "v"(T));
+    if (k >= 2) {
+      unsigned long long co;  // the carry-out (dead)
+      if (C - 1 - (k - 2) >= 32)
+        asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(hi), "=s"(co) : "s"(s[k - 2]));
+      else
+        asm volatile("v_addc_co_u32_e64 %0, %1, %0, %0, %2" : "+v"(lo), "=s"(co) : "s"(s[k - 2]));
+    }
+  }
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -335,10 +345,13 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
         vm = 0;
 #pragma unroll
         for (int i = 0; i < G; i++) vm |= (u_lo + i * D >= 0 && u_lo + i * D < W) ? (jm << (i * G)) : 0ull;
-      }
-      float lmax = -INFINITY;
+        // out-of-image candidates scored clamped window pixels: they take no part in the level's best (nor survive)
 #pragma unroll
-      for (int c = 0; c < G * G; c++) lmax = fmaxf(lmax, ((vm >> c) & 1ull) ? a[c] : -INFINITY);
+        for (int c = 0; c < G * G; c++) a[c] = ((vm >> c) & 1ull) ? a[c] : -INFINITY;
+      }
+      float lmax = a[0];
+#pragma unroll
+      for (int c = 1; c < G * G; c++) lmax = fmaxf(lmax, a[c]);
       const float T = fmaxf((float)max_score - t.bq, lmax - 2.0f * t.bq);
       uint64_t m = screen_mask(a, T);
       if (!t.sok) m = ~0ull;
