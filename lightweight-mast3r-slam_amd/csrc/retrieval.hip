@@ -174,7 +174,10 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
   auto stage_b = [&](int s, uint4* dst) {
     for (int i = w; i < RQ_QU / 64; i += RQ_THREADS / 64) {
       const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(rq_lptr)&dst[i * 64]);
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(qa + (size_t)s * RQ_QU + i * 64)
+      // one wait state between the M0 write and the LDS DMA that reads it (CDNA3/4 manually inserted wait states;
+      // the compiler's own global_load_lds sequences keep one instruction there)
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0),
+                   "v"(qa + (size_t)s * RQ_QU + i * 64)
                    : "memory");  // m0 is reserved (never allocated) by the compiler: no clobber needed
     }
   };
