@@ -261,11 +261,14 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   const int x_lo = mnu - RD, x_hi = mxu + RD, y_lo = mnv - RD, y_hi = mxv + RD;
   const int wx0 = (x_hi - x_lo + 1 <= RT_COLS) ? x_lo : ((x_lo + x_hi) >> 1) - RT_COLS / 2;
   const int wy0 = (y_hi - y_lo + 1 <= RT_ROWS) ? y_lo : ((y_lo + y_hi) >> 1) - RT_ROWS / 2;
-  const int nrows = min(RT_ROWS, y_hi - wy0 + 1);
+  // rows and columns actually filled: the bbox cover, clipped to the window (a fine level's cover is ~40 of the 64
+  // columns: the fill, bound by L2 -> LDS bandwidth, moves only those)
+  const int nrows = min(RT_ROWS, y_hi - wy0 + 1), ncols = min(RT_COLS, x_hi - wx0 + 1);
+  const bool col_in = lane < ncols;
   const int gx = min(max(wx0 + lane, 0), W - 1);
   const int u_lo = cu - RD, v_lo = cv - RD;
   const int bx = u_lo - wx0, by = v_lo - wy0;  // window coordinates of candidate (0, 0)
-  const bool lane_in = active && bx >= 0 && bx + 2 * RD < RT_COLS && by >= 0 && by + 2 * RD < nrows;
+  const bool lane_in = active && bx >= 0 && bx + 2 * RD < ncols && by >= 0 && by + 2 * RD < nrows;
   const bool outl = active && !lane_in;
   const uint64_t om = __ballot(outl);
 #ifdef M3S_REFINE_STATS
@@ -327,7 +330,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       for (int y = wid; y < nrows; y += 4) {
         const int gy = min(max(wy0 + y, 0), H - 1);
         const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
-        __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+        if (col_in) __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
       }
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -394,7 +397,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
       const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
-      __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+      if (col_in) __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
     }
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
