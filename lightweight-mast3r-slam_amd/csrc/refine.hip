@@ -37,6 +37,11 @@ namespace m3s {
 #define RT_TH 8
 #define RT_COLS 64
 #define RT_ROWS 40  // 40 x 64 x 16 B = 40 KiB per block: four blocks per CU
+// packed window (SCREEN, d = 1): all three chunk planes resident at once, 3 x 17 rows x 48 columns x 16 B = 38.25 KiB
+// (the d = 1 cover is 16 x 39-40 on 97 % of the synthetic 512x512 tiles, scripts/refine_window_stats.py)
+#define RT_PCOLS 48
+#define RT_PROWS 17
+#define RT_PPLANE (RT_PROWS * RT_PCOLS)
 
 typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
@@ -121,7 +126,7 @@ __device__ __forceinline__ void score_chunk(const uint4* base, const h2* q4, h1*
 //   * After the first level the centre candidate (3,3) is the last winner (its score IS the running max) or the
 //     start pixel that did not beat +0: it never wins a strict '>' and is dropped from the survivors.
 //   * |q| cmax > 16384 (overflow range) or non-finite: every in-image candidate survives (exact for all).
-template <int D>
+template <int D, int STRIDE = RT_COLS>
 __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, float* a) {
   constexpr int G = 7;
 #pragma unroll
@@ -129,7 +134,7 @@ __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, fl
     // the column's 7 candidate reads in flight together (one LDS latency per column, not per candidate)
     uint4 c[G];
 #pragma unroll
-    for (int j = 0; j < G; j++) c[j] = base[j * D * RT_COLS + i * D];
+    for (int j = 0; j < G; j++) c[j] = base[j * D * STRIDE + i * D];
 #pragma unroll
     for (int j = 0; j < G; j++) {
       const h2* cv = reinterpret_cast<const h2*>(&c[j]);
@@ -214,6 +219,28 @@ __device__ __forceinline__ void exact_survivors(const h1* __restrict__ img, int 
   }
 }
 
+// the packed window's variant: the survivors' three chunks are read from the resident LDS planes (base = candidate
+// (0,0) of this lane in plane 0), no L2 round trip; same ascending order, same strict '>'
+template <int D>
+__device__ __forceinline__ void exact_survivors_lds(const uint4* base, const h2* q, uint64_t m, h1& max_score,
+                                                    int& bi) {
+  while (m != 0) {
+    const int c = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int i = c / 7, j = c - 7 * i;
+    const uint4* p = base + j * D * RT_PCOLS + i * D;
+    const uint4 c0 = p[0], c1 = p[RT_PPLANE], c2 = p[2 * RT_PPLANE];
+    h1 sc = (h1)0.0f;
+    add8(sc, &q[0], c0);
+    add8(sc, &q[4], c1);
+    add8(sc, &q[8], c2);
+    if (sc > max_score) {
+      max_score = sc;
+      bi = c;
+    }
+  }
+}
+
 struct TileCtx {
   const h1* img;
   int H, W, lane, wid, u_pix, v_pix;
@@ -259,11 +286,14 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   }
   // window placement: exact bbox cover when it fits, else centred on the bbox
   const int x_lo = mnu - RD, x_hi = mxu + RD, y_lo = mnv - RD, y_hi = mxv + RD;
-  const int wx0 = (x_hi - x_lo + 1 <= RT_COLS) ? x_lo : ((x_lo + x_hi) >> 1) - RT_COLS / 2;
-  const int wy0 = (y_hi - y_lo + 1 <= RT_ROWS) ? y_lo : ((y_lo + y_hi) >> 1) - RT_ROWS / 2;
+  bool packed = false;  // block-uniform: every input is
+  if constexpr (SCREEN && D == 1) packed = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_PROWS;
+  const int wc = packed ? RT_PCOLS : RT_COLS, wr = packed ? RT_PROWS : RT_ROWS;
+  const int wx0 = (x_hi - x_lo + 1 <= wc) ? x_lo : ((x_lo + x_hi) >> 1) - wc / 2;
+  const int wy0 = (y_hi - y_lo + 1 <= wr) ? y_lo : ((y_lo + y_hi) >> 1) - wr / 2;
   // rows and columns actually filled: the bbox cover, clipped to the window (a fine level's cover is ~40 of the 64
   // columns: the fill, bound by L2 -> LDS bandwidth, moves only those)
-  const int nrows = min(RT_ROWS, y_hi - wy0 + 1), ncols = min(RT_COLS, x_hi - wx0 + 1);
+  const int nrows = min(wr, y_hi - wy0 + 1), ncols = min(wc, x_hi - wx0 + 1);
   const bool col_in = lane < ncols;
   const int gx = min(max(wx0 + lane, 0), W - 1);
   const int u_lo = cu - RD, v_lo = cv - RD;
@@ -323,21 +353,45 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #pragma unroll
     for (int c = 0; c < G * G; c++) a[c] = 0.0f;
     __syncthreads();  // the reduction scratch aliases the window: its readers are done
-#pragma unroll
-    for (int chunk = 0; chunk < F / 8; chunk++) {
-      if (chunk) __syncthreads();
+    if (packed) {  // (d = 1 only) the three chunk planes in one fill
 #ifndef RT_NOLOAD
-      for (int y = wid; y < nrows; y += 4) {
+      for (int r = wid; r < 3 * nrows; r += 4) {
+        const int chunk = r >= 2 * nrows ? 2 : (r >= nrows ? 1 : 0), y = r - chunk * nrows;
         const int gy = min(max(wy0 + y, 0), H - 1);
         const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
-        if (col_in) __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+        if (col_in)
+          __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off),
+                                           (lvoid_t)&lds[chunk * RT_PPLANE + y * RT_PCOLS], 16, 0, 0);
       }
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 #ifndef RT_NOCOMP
-      if (lane_in) screen_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], a);
+      if (lane_in) {
+        const int b0 = by * RT_PCOLS + bx;
+        screen_chunk<D, RT_PCOLS>(&lds[b0], &q[0], a);
+        screen_chunk<D, RT_PCOLS>(&lds[RT_PPLANE + b0], &q[4], a);
+        screen_chunk<D, RT_PCOLS>(&lds[2 * RT_PPLANE + b0], &q[8], a);
+      }
 #endif
+    } else {
+#pragma unroll
+      for (int chunk = 0; chunk < F / 8; chunk++) {
+        if (chunk) __syncthreads();
+#ifndef RT_NOLOAD
+        for (int y = wid; y < nrows; y += 4) {
+          const int gy = min(max(wy0 + y, 0), H - 1);
+          const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
+          if (col_in)
+            __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
+        }
+#endif
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#ifndef RT_NOCOMP
+        if (lane_in) screen_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], a);
+#endif
+      }
     }
     if (lane_in) {
       uint64_t vm = (1ull << (G * G)) - 1ull;  // in-image candidates
@@ -378,7 +432,10 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       m = 0;
 #endif
       int bi = -1;
-      exact_survivors<D, PLANAR>(t.img, H, W, q, u_lo, v_lo, m, max_score, bi);
+      if (packed)
+        exact_survivors_lds<D>(&lds[by * RT_PCOLS + bx], q, m, max_score, bi);
+      else
+        exact_survivors<D, PLANAR>(t.img, H, W, q, u_lo, v_lo, m, max_score, bi);
       if (bi >= 0) {
         cu = u_lo + (bi / G) * D;
         cv = v_lo + (bi % G) * D;
