@@ -42,6 +42,10 @@ namespace m3s {
 #define RT_PCOLS 48
 #define RT_PROWS 17
 #define RT_PPLANE (RT_PROWS * RT_PCOLS)
+// double-buffered window (SCREEN, d = 2): two 26-row x 48-column chunk buffers (2 x 19.5 KiB), chunk c + 1 streams in
+// while chunk c is screened (the d = 2 cover is 23 x 45-47 on 97.6 % of the synthetic 512x512 tiles)
+#define RT_DROWS 26
+#define RT_DBUF (RT_DROWS * RT_PCOLS)
 
 typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
@@ -219,6 +223,16 @@ __device__ __forceinline__ void exact_survivors(const h1* __restrict__ img, int 
   }
 }
 
+// LDS DMA of one window row (64 lanes x 16 B) by inline asm, for the double-buffered window: the compiler treats a
+// global_load_lds as an LDS store of unknown extent and drains it (vmcnt(0)) before the next ds_read, which would
+// serialise the fill of chunk c + 1 behind the screen of chunk c; the explicit vmcnt(0) + barrier order it instead.
+// One wait state between the M0 write and the DMA (the compiler's own sequences keep one there too).
+// lds_addr: the row's LDS byte address (wave-uniform)
+__device__ __forceinline__ void lds_dma_row(const h1* g, unsigned lds_addr) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(g) : "memory");
+}
+
 // the packed window's variant: the survivors' three chunks are read from the resident LDS planes (base = candidate
 // (0,0) of this lane in plane 0), no L2 round trip; same ascending order, same strict '>'
 template <int D>
@@ -248,6 +262,7 @@ struct TileCtx {
   int bn;       // batch * N + pixel
   int4* olist;  // deferred-pixel list (nullable: score outliers in place)
   int* ocount;
+  unsigned lds_addr;  // LDS byte address of the window (the block's __shared__ array)
   float bq;      // SCREEN: this lane's bound B (0.0125 |q| cmax + 2^-18)
   bool sok;      // SCREEN: the bound is usable (|q| cmax <= 16384 and finite)
 };
@@ -286,9 +301,10 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   }
   // window placement: exact bbox cover when it fits, else centred on the bbox
   const int x_lo = mnu - RD, x_hi = mxu + RD, y_lo = mnv - RD, y_hi = mxv + RD;
-  bool packed = false;  // block-uniform: every input is
+  bool packed = false, dbuf = false;  // block-uniform: every input is
   if constexpr (SCREEN && D == 1) packed = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_PROWS;
-  const int wc = packed ? RT_PCOLS : RT_COLS, wr = packed ? RT_PROWS : RT_ROWS;
+  if constexpr (SCREEN && D == 2) dbuf = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_DROWS;
+  const int wc = (packed || dbuf) ? RT_PCOLS : RT_COLS, wr = packed ? RT_PROWS : (dbuf ? RT_DROWS : RT_ROWS);
   const int wx0 = (x_hi - x_lo + 1 <= wc) ? x_lo : ((x_lo + x_hi) >> 1) - wc / 2;
   const int wy0 = (y_hi - y_lo + 1 <= wr) ? y_lo : ((y_lo + y_hi) >> 1) - wr / 2;
   // rows and columns actually filled: the bbox cover, clipped to the window (a fine level's cover is ~40 of the 64
@@ -373,6 +389,39 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
         screen_chunk<D, RT_PCOLS>(&lds[RT_PPLANE + b0], &q[4], a);
         screen_chunk<D, RT_PCOLS>(&lds[2 * RT_PPLANE + b0], &q[8], a);
       }
+#endif
+    } else if (dbuf) {  // (d = 2 only) chunk c + 1 lands in the other buffer while chunk c is screened
+      auto fill = [&](int chunk, int buf) {
+#ifndef RT_NOLOAD
+        for (int y = wid; y < nrows; y += 4) {
+          const int gy = min(max(wy0 + y, 0), H - 1);
+          const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
+          if (col_in) lds_dma_row(rowp + lane_off, t.lds_addr + (unsigned)(buf + y * RT_PCOLS) * 16u);
+        }
+#endif
+      };
+      const int b0 = by * RT_PCOLS + bx;
+      fill(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the same wait as a builtin: the compiler's wait model (blind to the asm) learns that none of its own loads
+      // (a previous level's survivor loads, spill reloads) is still in flight, so it places no vmcnt(0) of its own
+      // after fill(1), which would drain the DMA with them
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+      __syncthreads();
+      fill(1, RT_DBUF);
+#ifndef RT_NOCOMP
+      if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[b0], &q[0], a);
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // chunk 1 landed; every wave is done with buffer 0
+      fill(2, 0);
+#ifndef RT_NOCOMP
+      if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[RT_DBUF + b0], &q[4], a);
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#ifndef RT_NOCOMP
+      if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[b0], &q[8], a);
 #endif
     } else {
 #pragma unroll
@@ -545,6 +594,7 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
   }
   t.olist = olist;
   t.ocount = ocount;
+  t.lds_addr = (unsigned)(uintptr_t)(lvoid_t)lds;
   bool active = t.u_pix < W && t.v_pix < H;
   const int N = H * W;
   const size_t bn = (size_t)b * N + (size_t)t.v_pix * W + t.u_pix;
