@@ -10,8 +10,11 @@
 //   * Once per tile the block estimates the tile's flow (mean initial centre displacement); per level
 //     it takes the bbox of the centres within 16 px of it, places a 64-column x 40-row window over
 //     bbox +- 3d and streams D11 (f16) into LDS in three 8-channel chunks (16 B / px) with
-//     global_load_lds — one wave-instruction per window row. Four resident blocks per CU hide each other's fill latency
-//     (measured: faster than double-buffering at two blocks per CU).
+//     global_load_lds — one wave-instruction per window row, only the cover's columns. Four resident blocks per CU
+//     hide each other's fill latency (measured: faster than double-buffering at two blocks per CU). The fine levels'
+//     covers are small enough for other layouts of the same 40 KiB (bound-screened path): at d = 2 two 26 x 48
+//     chunk buffers (chunk c + 1 streams in while chunk c is screened), at d = 1 all three chunk planes of a 17 x 48
+//     window in one fill, the survivors then rescored from LDS.
 //   * Levels are specialised on d, so every candidate read is one ds_read_b128 with an immediate
 //     offset from a single per-lane base; the 49 running half sums live in registers across the
 //     three chunks (the sum stays sequential over k = 0..23: c10::Half step rounding unchanged).
@@ -259,6 +262,7 @@ struct TileCtx {
   const h1* img;
   int H, W, lane, wid, u_pix, v_pix;
   int fu, fv;   // tile flow estimate: mean initial centre displacement (fixed for all levels)
+  int tcu, tcv; // tile centre + flow estimate: the window's centre when the centres' cover does not fit
   int bn;       // batch * N + pixel
   int4* olist;  // deferred-pixel list (nullable: score outliers in place)
   int* ocount;
@@ -299,14 +303,17 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     mnu = mxu = 0;
     mnv = mxv = 0;
   }
-  // window placement: exact bbox cover when it fits, else centred on the bbox
+  // window placement: exact bbox cover when it fits, else centred on the tile's centre displaced by its flow
+  // estimate. A cover that does not fit is mostly a tight cluster plus a few far centres at one end: centring on the
+  // bbox middle deferred the cluster itself (d = 4 on the synthetic 512x512 pair: 1502 deferred lanes against 54,
+  // scripts/refine_window_stats.py)
   const int x_lo = mnu - RD, x_hi = mxu + RD, y_lo = mnv - RD, y_hi = mxv + RD;
   bool packed = false, dbuf = false;  // block-uniform: every input is
   if constexpr (SCREEN && D == 1) packed = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_PROWS;
   if constexpr (SCREEN && D == 2) dbuf = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_DROWS;
   const int wc = (packed || dbuf) ? RT_PCOLS : RT_COLS, wr = packed ? RT_PROWS : (dbuf ? RT_DROWS : RT_ROWS);
-  const int wx0 = (x_hi - x_lo + 1 <= wc) ? x_lo : ((x_lo + x_hi) >> 1) - wc / 2;
-  const int wy0 = (y_hi - y_lo + 1 <= wr) ? y_lo : ((y_lo + y_hi) >> 1) - wr / 2;
+  const int wx0 = (x_hi - x_lo + 1 <= wc) ? x_lo : t.tcu - wc / 2;
+  const int wy0 = (y_hi - y_lo + 1 <= wr) ? y_lo : t.tcv - wr / 2;
   // rows and columns actually filled: the bbox cover, clipped to the window (a fine level's cover is ~40 of the 64
   // columns: the fill, bound by L2 -> LDS bandwidth, moves only those)
   const int nrows = min(wr, y_hi - wy0 + 1), ncols = min(wc, x_hi - wx0 + 1);
@@ -627,6 +634,8 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
     const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
     t.fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
     t.fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
+    t.tcu = tx * RT_TW + RT_TW / 2 + t.fu;
+    t.tcv = ty * RT_TH + RT_TH / 2 + t.fv;
   }
   t.bq = 0.0f;
   t.sok = false;

@@ -63,6 +63,24 @@ def main():
               f"non-inlier px {int((~inl).sum())}")
         for rlim, clim in ((17, 48), (26, 48), (20, 64), (40, 64)):
             print(f"      fits rows<={rlim} cols<={clim}: {np.mean((rows <= rlim) & (cols <= clim)) * 100:.1f}% of tiles")
+        # deferred lanes of the 40 x 64 window when the cover does not fit, by placement rule: bbox middle (shipped),
+        # mean inlier centre, tile centre + flow estimate
+        RD = 3 * d
+        x_lo, x_hi, y_lo, y_hi = mnu - RD, mxu + RD, mnv - RD, mxv + RD
+        cntin = np.bincount(tile[inl], minlength=ntiles).clip(1)
+        mu = np.bincount(tile[inl], cu[inl], ntiles) / cntin
+        mv = np.bincount(tile[inl], cv[inl], ntiles) / cntin
+        tcu = (np.arange(ntiles) % ((W + TW - 1) // TW)) * TW + TW // 2 + fu
+        tcv = (np.arange(ntiles) // ((W + TW - 1) // TW)) * TH + TH // 2 + fv
+        for name, cx, cy in (("bbox-mid", (x_lo + x_hi) >> 1, (y_lo + y_hi) >> 1),
+                             ("mean", np.round(mu).astype(np.int64), np.round(mv).astype(np.int64)),
+                             ("flow", tcu, tcv)):
+            wx0 = np.where(x_hi - x_lo + 1 <= 64, x_lo, cx - 32)
+            wy0 = np.where(y_hi - y_lo + 1 <= 40, y_lo, cy - 20)
+            bx = cu - RD - wx0[tile]
+            by = cv - RD - wy0[tile]
+            lin = (bx >= 0) & (bx + 2 * RD < 64) & (by >= 0) & (by + 2 * RD < 40)
+            print(f"      placement {name:8s}: deferred lanes {int((~lin).sum())}")
         # one level (fp32 scores; scan order u outer, v inner; strict '>')
         off = np.arange(-3, 4) * d
         cand_u = np.clip(cu[:, None, None] + off[:, None, None].T.reshape(1, 7, 1), 0, W - 1)
