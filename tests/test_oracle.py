@@ -69,8 +69,9 @@ def test_tracker_restatement_matches_reference(golden, mode):
     else:
         Tf, Tr, _ = O.track_calib(g["Xf_c"], g["Xk"], g["T_WCf"][0], g["T_WCk"][0], g["Qk"], g["valid"], g["meas"],
                                   g["vmeas"], g["K"], (H, W))
-    np.testing.assert_allclose(Tf, g[f"{mode}_T_WCf"][0], atol=2e-5)
-    np.testing.assert_allclose(Tr, g[f"{mode}_T_CkCf"][0], atol=2e-5)
+    # the pose contract (1e-5); measured 1.4e-6 (rays) and 1.0e-7 (calib) against the reference run's poses
+    np.testing.assert_allclose(Tf, g[f"{mode}_T_WCf"][0], atol=1e-5)
+    np.testing.assert_allclose(Tr, g[f"{mode}_T_CkCf"][0], atol=1e-5)
 
 
 @pytest.mark.parametrize("mode", ["points", "rays", "calib"])
