@@ -34,7 +34,7 @@ hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int
 hipError_t m3s_launch_refine_lin(const void*, const float*, const int*, int64_t*, int, int, int, int, int, int,
                                  void*, int*, const float*, hipStream_t);
 hipError_t m3s_launch_track_setup(const TrackArgs*, const TrackParams*, hipStream_t);
-hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, hipStream_t);
+hipError_t m3s_launch_track_iters(const TrackArgs*, const TrackParams*, int, int, int, int, hipStream_t);
 hipError_t m3s_launch_fuse(const TrackArgs*, int, const FuseArgs*, int, int, const TrackPublish*, hipStream_t);
 hipError_t m3s_launch_track_init(const TrackArgs*, const float*, const float*, int, hipStream_t);
 int m3s_track_max_parts(void);
@@ -453,7 +453,10 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
     clean = n16;
   }
-  {
+  // M3S_TRACK_FOLD_SETUP=1: the per-point setup runs inside the GN launch's first iteration (no track_setup launch)
+  const char* fold_env = getenv("M3S_TRACK_FOLD_SETUP");
+  const int fold = fold_env != nullptr && fold_env[0] == '1';
+  if (!fold) {
     Span sp("track_setup", s);
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
   }
@@ -465,7 +468,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   TrackPublish pub{mirror, a.tick + M3S_TRACK_PUBLISH_TICKET, ++gen};
   {
     Span sp("gn_iters", s);
-    HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, p.max_iters, 0, s), "track iterate launch");
+    HIP_TRY(m3s_launch_track_iters(&a, &p, nparts, p.max_iters, 0, fold, s), "track iterate launch");
   }
   // keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) after a successful solve (tracker.py:91-101): enqueued
   // before the readback, it runs only if the solve finished with a pose

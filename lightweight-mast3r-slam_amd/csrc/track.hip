@@ -85,30 +85,29 @@ __device__ void track_state_init(TrackState* st, const float* T_WCf, const float
 }
 
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n == 0) track_state_init(a.state, a.T_WCf, a.T_WCk);
-  int v_opt = 0, v_kf = 0;
-  if (n < p.N && p.direct) {  // opt_pose_* surface: Qff = Qk, valid_match = valid, Xf pre-gathered
+// the 32-byte GN record of point n < N (r0, r1), its validity for the solve (v_opt) and for the keyframe stats
+// (v_kf), and the unique-match byte map entry
+__device__ __forceinline__ void setup_point(const TrackArgs& a, const TrackParams& p, int n, float4& r0, float4& r1,
+                                            int& v_opt, int& v_kf) {
+  if (p.direct) {  // opt_pose_* surface: Qff = Qk, valid_match = valid, Xf pre-gathered
     const float qk = a.Qff[n];
     const bool valid_opt = a.valid_match[n] != 0;
     v_opt = valid_opt;
     v_kf = valid_opt;
     const float sq = valid_opt ? sqrtf(qk) : 0.0f;
-    float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
     const float* Xf = a.Xf + (size_t)n * 3;
     if (p.mode == 0) {
       const float* Xk = a.Xk + (size_t)n * 3;
       const float d = sqrtf(Xk[0] * Xk[0] + Xk[1] * Xk[1] + Xk[2] * Xk[2]);
       const float di = 1.0f / d;
-      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
-      rec[1] = make_float4(di * Xk[1], di * Xk[2], d, sq);
+      r0 = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
+      r1 = make_float4(di * Xk[1], di * Xk[2], d, sq);
     } else {
       const float* m = a.meas_k + (size_t)n * 3;
-      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], m[0]);
-      rec[1] = make_float4(m[1], m[2], a.valid_meas[n] ? 1.0f : 0.0f, sq);
+      r0 = make_float4(Xf[0], Xf[1], Xf[2], m[0]);
+      r1 = make_float4(m[1], m[2], a.valid_meas[n] ? 1.0f : 0.0f, sq);
     }
-  } else if (n < p.N) {
+  } else {
     const int64_t i = a.idx[n];
     const float qk = sqrtf(a.Qff[i] * a.Qkf[n]);
     const float cf = a.Cf[i] / p.Nf;  // frame.get_average_conf(): C / N
@@ -117,16 +116,15 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
     const bool valid_opt = vm && (cf > p.C_conf) && (ck > p.C_conf) && (qk > p.Q_conf);
     v_opt = valid_opt;
     v_kf = vm && (qk > p.Q_conf);
-    if (vm) a.flags[i] = 1;  // benign same-value races; popcounted by the first GN launch
+    if (vm) a.flags[i] = 1;  // benign same-value races; popcounted by the fuse launch
     const float sq = valid_opt ? sqrtf(qk) : 0.0f;
-    float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
     const float* Xf = a.Xf + i * 3;
     const float* Xk = a.Xk + (size_t)n * 3;
     if (p.mode == 0) {  // rays: [Xf[idx], rd_k = (Xk/|Xk|, |Xk|), sqrtQ*valid]
       const float d = sqrtf(Xk[0] * Xk[0] + Xk[1] * Xk[1] + Xk[2] * Xk[2]);
       const float di = 1.0f / d;
-      rec[0] = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
-      rec[1] = make_float4(di * Xk[1], di * Xk[2], d, sq);
+      r0 = make_float4(Xf[0], Xf[1], Xf[2], di * Xk[0]);
+      r1 = make_float4(di * Xk[1], di * Xk[2], d, sq);
     } else {  // calib: constrain_points_to_ray at pixel idx, meas_k = [u_n, v_n, log z_k]
       const int i32 = (int)i, vi = i32 / p.W;  // 32-bit: i < H*W
       const float uf = (float)(i32 - vi * p.W), vf = (float)vi;
@@ -137,9 +135,22 @@ __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackPara
       const bool vmeas = zk > p.depth_eps;
       const int vnn = n / p.W;
       const float un = (float)(n - vnn * p.W), vn = (float)vnn;
-      rec[0] = make_float4(xc, yc, zf, vmeas ? un : 0.0f);
-      rec[1] = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
+      r0 = make_float4(xc, yc, zf, vmeas ? un : 0.0f);
+      r1 = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
     }
+  }
+}
+
+__global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n == 0) track_state_init(a.state, a.T_WCf, a.T_WCk);
+  int v_opt = 0, v_kf = 0;
+  if (n < p.N) {
+    float4 r0, r1;
+    setup_point(a, p, n, r0, r1, v_opt, v_kf);
+    float4* rec = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
+    rec[0] = r0;
+    rec[1] = r1;
   }
   // block-reduce the two counters into one packed 64-bit add on this block's XCD shard: one counter word
   // for all 1024 blocks serialises the adds (~11 ns each, MI355X_MICROARCH.md "fanin")
@@ -453,20 +464,45 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
 //      system, retracts and tests convergence itself: the same instructions on the same bytes, so every block
 //      holds the same T bit for bit, and no broadcast hop or serial last-block tail sits on the chain.
 // Spins are bounded: a stalled hand-off ends the frame with status STALLED (the host raises), never a hang.
+//
+// SETUP (folded setup, M3S_TRACK_FOLD_SETUP=1): no track_setup launch. Every block derives the initial T_CkCf
+// itself (track_state_init's arithmetic), builds its points' records in the first iteration (setup_point: the
+// first round into registers, later rounds also into the record buffer for the later iterations), and adds its
+// valid counts to the shard counters before its iteration-0 ticket; the skip test (tracker.py:67-70) then reads the
+// counters after the iteration-0 hand-off, before the first solve, and block 0 writes the whole final state.
+template <bool SETUP>
 __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackParams p) {
   TrackState* st = a.state;
-  if (st->done) return;
-  const unsigned long long counts = track_counts(a.cnt);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the host readback
-    st->n_valid_opt = (int)(unsigned)counts;
-    st->n_valid_kf = (int)(unsigned)(counts >> 32);
-  }
-  if (track_skipped((unsigned)counts, p)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->status = M3S_TRACK_SKIPPED;
-      st->done = 1;
+  float T[8];
+  double old;  // the convergence test's previous cost (inf before the first solve)
+  unsigned long long counts = 0;
+  if constexpr (SETUP) {
+    float Tk[8], Tf[8], Ti[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      Tk[c] = a.T_WCk[c];
+      Tf[c] = a.T_WCf[c];
     }
-    return;
+    sim3_inv(Tk, Ti);
+    sim3_mul_norm(Ti, Tf, T);
+    old = __builtin_inf();
+  } else {
+    if (st->done) return;
+    counts = track_counts(a.cnt);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the host readback
+      st->n_valid_opt = (int)(unsigned)counts;
+      st->n_valid_kf = (int)(unsigned)(counts >> 32);
+    }
+    if (track_skipped((unsigned)counts, p)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->status = M3S_TRACK_SKIPPED;
+        st->done = 1;
+      }
+      return;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) T[c] = st->T[c];
+    old = st->old_cost;
   }
   __shared__ double s_w[GN_THREADS / 64][64];  // per-wave totals (wave_sum36 lanes)
   __shared__ double s_sum[GN_NSUM];
@@ -474,15 +510,13 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   __shared__ double s_shard[M3S_TRACK_SHARDS][GN_NSUM];
   __shared__ int s_last, s_stop, s_fin;
   __shared__ float s_T[8];
+  __shared__ unsigned long long s_cnt[GN_THREADS / 64];  // SETUP: per-wave valid counts
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned nblk = gridDim.x;
   const int shard = blockIdx.x % M3S_TRACK_SHARDS;
   const int nsh = (int)min(nblk, (unsigned)M3S_TRACK_SHARDS);
   const unsigned per = (nblk - shard + M3S_TRACK_SHARDS - 1) / M3S_TRACK_SHARDS;  // blocks in this shard
-  float T[8];
-#pragma unroll
-  for (int c = 0; c < 8; c++) T[c] = st->T[c];
-  double old = st->old_cost;  // the convergence test's previous cost (inf before the first solve)
+  const float T0[8] = {T[0], T[1], T[2], T[3], T[4], T[5], T[6], T[7]};  // SETUP: a skipped frame keeps it
   int iters_done = 0, status = M3S_TRACK_RUNNING;
   double cost = 0.0;
   const float4* rec = reinterpret_cast<const float4*>(a.rec);
@@ -491,11 +525,23 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   // only the poses change between iterations
   const int n00 = blockIdx.x * GN_THREADS + threadIdx.x;
   float4 c0[GN_PPT], c1[GN_PPT];
+  int v_opt = 0, v_kf = 0;  // SETUP: this thread's valid counts (iteration 0)
 #pragma unroll
   for (int u = 0; u < GN_PPT; u++) {
-    const int n = min(n00 + u * stride, p.N - 1);
-    c0[u] = rec[2 * (size_t)n];
-    c1[u] = rec[2 * (size_t)n + 1];
+    if constexpr (SETUP) {
+      const int n = n00 + u * stride;
+      c0[u] = c1[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (n < p.N) {
+        int vo = 0, vk = 0;
+        setup_point(a, p, n, c0[u], c1[u], vo, vk);
+        v_opt += vo;
+        v_kf += vk;
+      }
+    } else {
+      const int n = min(n00 + u * stride, p.N - 1);
+      c0[u] = rec[2 * (size_t)n];
+      c1[u] = rec[2 * (size_t)n + 1];
+    }
   }
   gu32* gran = (gu32*)(a.tick + M3S_TRACK_GRANULES);  // [2 parities][8 shards][72] x {half, tag}
   for (int it = 0; it < p.max_iters; it++) {
@@ -514,8 +560,21 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
 #pragma unroll
       for (int u = 0; u < GN_PPT; u++) {
         const int n = min(n0 + u * stride, p.N - 1);
-        r0[u] = rec[2 * (size_t)n];
-        r1[u] = rec[2 * (size_t)n + 1];
+        if (SETUP && it == 0) {  // built here, stored for the later iterations (read back by this same thread)
+          r0[u] = r1[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (n0 + u * stride < p.N) {
+            int vo = 0, vk = 0;
+            setup_point(a, p, n, r0[u], r1[u], vo, vk);
+            v_opt += vo;
+            v_kf += vk;
+            float4* w = reinterpret_cast<float4*>(a.rec) + 2 * (size_t)n;
+            w[0] = r0[u];
+            w[1] = r1[u];
+          }
+        } else {
+          r0[u] = rec[2 * (size_t)n];
+          r1[u] = rec[2 * (size_t)n + 1];
+        }
       }
 #pragma unroll
       for (int u = 0; u < GN_PPT; u++)
@@ -523,7 +582,19 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     }
     GN_STAMP(1);
     s_w[wid][lane] = wave_sum36(acc, lane);
+    if (SETUP && it == 0) {  // the wave's valid counts, packed (n_valid_kf << 32) | n_valid_opt like track_setup's
+      unsigned long long c = ((unsigned long long)(unsigned)v_kf << 32) | (unsigned)v_opt;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+      if (lane == 0) s_cnt[wid] = c;
+    }
     __syncthreads();
+    if (SETUP && it == 0 && threadIdx.x == 0) {  // before this block's ticket (the vmcnt(0) below drains it)
+      unsigned long long c = 0;
+#pragma unroll
+      for (int w = 0; w < GN_THREADS / 64; w++) c += s_cnt[w];
+      if (c) __hip_atomic_fetch_add(&a.cnt[16 * shard], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the block partial: 36 threads add the 4 waves' totals, store it write-through into this iteration's slot
     const int slot = it % GN_SLOTS;
     gdouble* part = (gdouble*)(a.partials + (size_t)slot * GN_MAX_BLOCKS * GN_PSTRIDE);
@@ -614,6 +685,23 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       for (int k = 1; k < nsh; k++) v += s_shard[k][c];
       s_sum[c] = v;
     }
+    if (SETUP && it == 0) {
+      // every block's counts were added before its iteration-0 ticket, and every shard sum seen above follows all
+      // of its shard's tickets: the counters are complete (device-scope loads)
+      if (threadIdx.x == 0) {
+        unsigned long long c = 0;
+#pragma unroll
+        for (int k = 0; k < M3S_TRACK_SHARDS; k++)
+          c += __hip_atomic_load(&a.cnt[16 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_cnt[0] = c;
+      }
+      __syncthreads();
+      counts = s_cnt[0];
+      if (track_skipped((unsigned)counts, p)) {
+        status = M3S_TRACK_SKIPPED;
+        break;
+      }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       const GnStep r = gn_step(p, s_sum, T, it, old);
@@ -634,7 +722,36 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   }
   // the final state, written by ONE block (plain stores of a single writer; the host and the fuse launch read it
   // after this launch); every block holds the same values
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (SETUP && blockIdx.x == 0 && threadIdx.x == 0) {  // the whole state: track_state_init + the GN launch's writes
+    TrackState v{};
+#pragma unroll
+    for (int c = 0; c < 8; c++) v.T_WCk[c] = a.T_WCk[c];
+    v.n_valid_opt = (int)(unsigned)counts;
+    v.n_valid_kf = (int)(unsigned)(counts >> 32);
+    v.done = 1;
+    v.status = status;
+    if (status == M3S_TRACK_SKIPPED) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) v.T[c] = T0[c];
+      v.old_cost = __builtin_inf();
+    } else {
+      v.iter = iters_done;
+      v.last_cost = cost;
+      v.old_cost = cost;
+#pragma unroll
+      for (int c = 0; c < 8; c++) v.T[c] = T[c];
+      if (status == M3S_TRACK_OK || status == M3S_TRACK_MAX_ITERS) {
+        sim3_mul_norm(v.T_WCk, T, v.T_WCf);  // T_WCf = T_WCk * T_CkCf
+        if (a.T_out != nullptr)
+          for (int c = 0; c < 8; c++) {
+            a.T_out[c] = v.T_WCf[c];
+            a.T_out[8 + c] = T[c];
+          }
+      }
+    }
+    *st = v;
+  }
+  if (!SETUP && blockIdx.x == 0 && threadIdx.x == 0) {
     st->iter = iters_done;
     st->last_cost = cost;
     st->old_cost = cost;
@@ -764,23 +881,31 @@ extern "C" int m3s_track_max_parts(void) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1;
   if (dev >= 0 && dev < 64 && cache[dev] > 0) return cache[dev];
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(m3s::gn_loop_kernel),
+  int per_cu = 0, per_cu_fold = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(m3s::gn_loop_kernel<false>),
+                                                   GN_THREADS, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_fold,
+                                                   reinterpret_cast<const void*>(m3s::gn_loop_kernel<true>),
                                                    GN_THREADS, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 1;
+  per_cu = per_cu_fold < per_cu ? per_cu_fold : per_cu;  // either variant's grid is fully resident
   const int n = per_cu * cus > 1 ? per_cu * cus : 1;
   if (dev >= 0 && dev < 64) cache[dev] = n;
   return n;
 }
 
-// one persistent launch runs every GN iteration (iters and chunk_id are kept for the call sites)
+// one persistent launch runs every GN iteration (iters and chunk_id are kept for the call sites); fold: the setup
+// runs inside it (gn_loop_kernel<true>, no track_setup launch before it)
 extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackParams* p, int nparts, int iters,
-                                             int chunk_id, hipStream_t s) {
+                                             int chunk_id, int fold, hipStream_t s) {
   (void)iters;
   (void)chunk_id;
   if (nparts < 1 || nparts > 256) return hipErrorInvalidValue;  // <= 32 blocks per XCD shard (the shard-last loads)
-  hipLaunchKernelGGL(m3s::gn_loop_kernel, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
+  if (fold)
+    hipLaunchKernelGGL(m3s::gn_loop_kernel<true>, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
+  else
+    hipLaunchKernelGGL(m3s::gn_loop_kernel<false>, dim3(nparts), dim3(GN_THREADS), 0, s, *a, *p);
   return hipGetLastError();
 }
 

@@ -297,3 +297,75 @@ def test_track_writes_fused_keyframe_into_shared_slot():
     finally:
         manager.shutdown()
         config["use_calib"] = False
+
+
+def _track_once(g, mode, H, W, cfg):
+    from m3s.tracker import FrameTracker
+
+    kf, frame, kfs, model = _setup(g, mode == "calib", H * W, H, W)
+    for k, v in cfg.items():
+        _mode_cfg(k, v)
+    tr = FrameTracker(model, kfs, "cuda")
+    out = tr.track(frame)
+    r = tr.last_result
+    res = None if r is None else (list(r.T_WCf), list(r.T_CkCf), r.cost, r.iters, r.status, r.n_valid_opt,
+                                  r.n_valid_kf, r.n_unique)
+    return (bool(out[0]), bool(out[2]), res, frame.T_WC.data.cpu().clone(), kf.X_canon.cpu().clone(),
+            kf.C.cpu().clone(), kf.N)
+
+
+@pytest.mark.parametrize("case", ["rays", "calib", "skip", "cholesky", "max_iters"])
+def test_track_folded_setup_bit_identical(golden, monkeypatch, case):
+    """M3S_TRACK_FOLD_SETUP=1 (setup inside the GN launch's first iteration, the skip test after its hand-off) gives
+    the separate-setup path's result bit for bit: pose, cost, iterations, status, counts, fused keyframe."""
+    from m3s.config import reset_config
+
+    g = golden("tracking_48x64.npz")
+    mode = "calib" if case == "calib" else "rays"
+    cfg = {"skip": {"Q_conf": 1e9}, "cholesky": {"min_match_frac": 0.0, "Q_conf": 1e9},
+           "max_iters": {"max_iters": 1}}.get(case, {})
+    outs = []
+    for fold in ("0", "1"):
+        monkeypatch.setenv("M3S_TRACK_FOLD_SETUP", fold)
+        reset_config()
+        outs.append(_track_once(g, mode, 48, 64, cfg))
+    a, b = outs
+    assert a[:3] == b[:3]
+    for x, y in zip(a[3:6], b[3:6]):
+        assert torch.equal(x, y)
+    assert a[6] == b[6]
+
+
+def test_track_folded_setup_full_size_bit_identical(monkeypatch):
+    """512x512 (every point in the GN launch's registers) and 640x480 (points past the first round: records built in
+    iteration 0 into the record buffer, read back later), folded vs separate setup, both modes."""
+    from m3s.config import config, reset_config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    for (H, W) in ((512, 512), (480, 640)):
+        P = make_pair(H, W, seed=2)
+        for calib in (False, True):
+            outs = []
+            for fold in ("0", "1"):
+                monkeypatch.setenv("M3S_TRACK_FOLD_SETUP", fold)
+                reset_config()
+                config["use_calib"] = calib
+                model = SyntheticModel([P], "cuda")
+                kf = Frame(0, (H, W))
+                kf.T_WC = Sim3.Identity(1, device="cuda")
+                kf.K = P["K"].cuda()
+                kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
+                kfs = Keyframes()
+                kfs.append(kf)
+                tr = FrameTracker(model, kfs, "cuda")
+                frame = Frame(1, (H, W), T_WC=Sim3.Identity(1, device="cuda"))
+                frame.K = P["K"].cuda()
+                tr.track(frame)
+                r = tr.last_result
+                outs.append(((r.cost, r.iters, r.status, r.n_valid_opt, r.n_valid_kf, r.n_unique),
+                             frame.T_WC.data.cpu(), kf.X_canon.cpu()))
+            assert outs[0][0] == outs[1][0], (H, W, calib)
+            assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2]), (H, W, calib)
