@@ -571,8 +571,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
 
 size_t ba_carve(Carver& c, int Kp, int N, int E, int chunks, BaArgs* a, size_t* es_off, void** blob) {
   const int nb = std::max(0, Kp - 1);
-  a->rec = c.take<float4>((size_t)E * N);  // worst case: a shard packs only its own edges
-  a->rec_n = c.take<float>((size_t)E * N);  // rays: |Xi| per record
+  // record slots (worst case: a shard packs only its own edges), each N records + the rays' N |Xi|
+  a->rec = c.take<float4>((size_t)E * ba_rec_slot_bytes(N) / 16);
   a->partials = c.take<double>((size_t)E * chunks * 36);
   *es_off = c.off;
   a->edge_sums = c.take<double>((size_t)E * 36);

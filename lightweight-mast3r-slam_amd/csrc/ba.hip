@@ -206,6 +206,11 @@ __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p
   }
 }
 
+// record slot s (m3s_ba.h ba_rec_slot_bytes): N records, then the rays' |Xi| at rec + N
+__device__ __forceinline__ float4* rec_of_slot(const BaArgs& a, int s, int N) {
+  return reinterpret_cast<float4*>(reinterpret_cast<char*>(a.rec) + (size_t)s * ba_rec_slot_bytes(N));
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack) {
   const int N = p.N;
@@ -213,10 +218,10 @@ __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int 
   for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
     const int t = (int)(o / N), k = (int)(o - (size_t)t * N);
     const int e = a.pack_list ? a.pack_list[t] : t;
-    const size_t r = (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N + k;
+    float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
     float n = 0.0f;
-    a.rec[r] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n);
-    if constexpr (MODE == BA_MODE_RAYS) a.rec_n[r] = n;
+    rec[k] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n);
+    if constexpr (MODE == BA_MODE_RAYS) reinterpret_cast<float*>(rec + N)[k] = n;
   }
 }
 
@@ -308,8 +313,8 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
 #pragma unroll
   for (int c = 0; c < 7; c++) v[c] = 0.0;
 #endif
-  float4* rec = a.rec + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;
-  float* rec_n = a.rec_n + (size_t)(a.rec_slot ? a.rec_slot[e] : e) * N;  // rays: |Xi|
+  float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
+  float* rec_n = reinterpret_cast<float*>(rec + N);  // rays: |Xi|
   const float* Xj_base = a.Xkf[jx];
   const int per = (N + p.chunks - 1) / p.chunks;
   const int k_begin = chunk * per;

@@ -31,6 +31,11 @@ struct BaKfCopy {
   float* copy;
 };
 
+// bytes of one record slot: N 16-B records, then N floats (rays: |Xi|) padded to 16 B. A slot's bytes sit at
+// slot * ba_rec_slot_bytes(N) whatever the plan's edge count: record reuse keeps slots across the plans of a growing
+// graph, and a region [all records | all |Xi|] would move its second part with the edge count
+__host__ __device__ inline size_t ba_rec_slot_bytes(int N) { return (size_t)16 * N + (size_t)4 * ((N + 3) & ~3); }
+
 struct BaArgs {
   float* Twc;            // (K,8) in/out
   const float* const* Xkf;  // (K) -> (N,3) keyframe points: rows of the stacked Xs, or each keyframe's X_canon
@@ -41,8 +46,8 @@ struct BaArgs {
   const int64_t* idx;    // (E,N) global edge rows
   const uint8_t* valid;  // (E,N)
   const float* Q;        // (E,N)
-  float4* rec;           // (slots, N) point records (ba_pack): {Xi | Xi/|Xi| (rays) | u_t, v_t, log z_i ; sqrt-weight}
-  float* rec_n;          // (slots, N) rays mode: |Xi| (the record holds the unit ray)
+  float4* rec;           // record slots (ba_rec_slot_bytes each): N point records {Xi | Xi/|Xi| (rays) | u_t, v_t,
+                         // log z_i ; sqrt-weight}, then (rays) N floats |Xi|
   const int* rec_slot;   // (E_local) record slot of each shard edge (record reuse across plans), or null: slot = edge
   const int* pack_list;  // (n_pack) shard edges the pack writes (the others kept their records), or null: all
   double* partials;      // (E_local*chunks, 36)
