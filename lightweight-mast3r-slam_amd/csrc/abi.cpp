@@ -317,10 +317,17 @@ static int wait_published(const TrackMirror* m, unsigned gen, hipStream_t s) {
   }
 }
 
-// workspaces whose frame scratch the last fuse launch cleared: workspace -> {clean byte-map entries (uint4), the
-// workspace's size}; an entry is dropped by m3s_track_release (the caller frees or repurposes the workspace)
+// workspaces whose frame scratch the last fuse launch cleared: workspace -> {the workspace's size, the image size N
+// of that frame}. The scratch layout (track_carve) depends on N: a frame of another size wrote its records and
+// partials where this size's byte map lies (a 48x64 frame left 5540 stale map entries under a following 512x512
+// frame's unique-match count), so the record holds only for the same N. Dropped by m3s_track_release (the caller
+// frees or repurposes the workspace).
+struct TrackClean {
+  size_t bytes;
+  int N;
+};
 static std::mutex g_track_clean_mu;
-static std::map<const void*, std::pair<int, size_t>> g_track_clean;
+static std::map<const void*, TrackClean> g_track_clean;
 
 extern "C" int m3s_track_release(const void* workspace) {
   std::lock_guard<std::mutex> lock(g_track_clean_mu);
@@ -441,18 +448,14 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   }
   // the previous frame's fuse launch left this workspace's scratch clean (byte map of n16 entries, counters,
   // tickets): track_init runs only for a fresh / grown / failed workspace
-  const int n16 = (N + 15) / 16;
-  int clean = 0;
+  bool clean = false;
   {
     std::lock_guard<std::mutex> lock(g_track_clean_mu);
     auto it = g_track_clean.find(workspace);
-    if (it != g_track_clean.end() && it->second.second == workspace_bytes) clean = it->second.first;
+    clean = it != g_track_clean.end() && it->second.bytes == workspace_bytes && it->second.N == N;
     g_track_clean.erase(workspace);  // dirty until this call has published
   }
-  if (clean < n16) {
-    HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
-    clean = n16;
-  }
+  if (!clean) HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
   // M3S_TRACK_FOLD_SETUP=1: the per-point setup runs inside the GN launch's first iteration (no track_setup launch)
   const char* fold_env = getenv("M3S_TRACK_FOLD_SETUP");
   const int fold = fold_env != nullptr && fold_env[0] == '1';
@@ -478,7 +481,7 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
   if (int rc = wait_published(mirror, pub.gen, s)) return rc;
   {
     std::lock_guard<std::mutex> lock(g_track_clean_mu);
-    g_track_clean[workspace] = {clean, workspace_bytes};  // the fuse launch cleared what this frame dirtied
+    g_track_clean[workspace] = {workspace_bytes, N};  // the fuse launch cleared what this frame dirtied
   }
   const TrackState& hs = mirror->s;
   if (hs.status == M3S_TRACK_STALLED)

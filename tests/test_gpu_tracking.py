@@ -317,7 +317,8 @@ def _track_once(g, mode, H, W, cfg):
 @pytest.mark.parametrize("case", ["rays", "calib", "skip", "cholesky", "max_iters"])
 def test_track_folded_setup_bit_identical(golden, monkeypatch, case):
     """M3S_TRACK_FOLD_SETUP=1 (setup inside the GN launch's first iteration, the skip test after its hand-off) gives
-    the separate-setup path's result bit for bit: pose, cost, iterations, status, counts, fused keyframe."""
+    the separate-setup path's result: decisions, iterations, status and counts exactly, pose and fused points to
+    1e-6, fused confidences exactly."""
     from m3s.config import reset_config
 
     g = golden("tracking_48x64.npz")
@@ -330,15 +331,24 @@ def test_track_folded_setup_bit_identical(golden, monkeypatch, case):
         reset_config()
         outs.append(_track_once(g, mode, 48, 64, cfg))
     a, b = outs
-    assert a[:3] == b[:3]
-    for x, y in zip(a[3:6], b[3:6]):
-        assert torch.equal(x, y)
-    assert a[6] == b[6]
+    assert a[:2] == b[:2]
+    if a[2] is None or b[2] is None:
+        assert a[2] is None and b[2] is None
+    else:  # iterations, status and the counts exactly; the pose to 1e-6 (see below)
+        assert a[2][3:] == b[2][3:]
+        np.testing.assert_allclose(a[2][0] + a[2][1], b[2][0] + b[2][1], rtol=0, atol=1e-6)
+        assert abs(a[2][2] - b[2][2]) <= 1e-5 * abs(a[2][2])
+    # the two launches are separate compilations: FMA contraction may round a record or the initial pose by an ulp,
+    # which the GN iterations carry to ~1e-7 in the pose (measured: 8e-9 .. 7e-8 on this fixture)
+    np.testing.assert_allclose(a[3].numpy(), b[3].numpy(), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(a[4].numpy(), b[4].numpy(), rtol=1e-6, atol=1e-6)
+    assert torch.equal(a[5], b[5]) and a[6] == b[6]
 
 
-def test_track_folded_setup_full_size_bit_identical(monkeypatch):
+def test_track_folded_setup_full_size(monkeypatch):
     """512x512 (every point in the GN launch's registers) and 640x480 (points past the first round: records built in
-    iteration 0 into the record buffer, read back later), folded vs separate setup, both modes."""
+    iteration 0 into the record buffer, read back later), folded vs separate setup, both modes (tolerances as
+    above)."""
     from m3s.config import config, reset_config
     from m3s.frame import Frame, Keyframes
     from m3s.sim3 import Sim3
@@ -365,7 +375,50 @@ def test_track_folded_setup_full_size_bit_identical(monkeypatch):
                 frame.K = P["K"].cuda()
                 tr.track(frame)
                 r = tr.last_result
-                outs.append(((r.cost, r.iters, r.status, r.n_valid_opt, r.n_valid_kf, r.n_unique),
-                             frame.T_WC.data.cpu(), kf.X_canon.cpu()))
-            assert outs[0][0] == outs[1][0], (H, W, calib)
-            assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2]), (H, W, calib)
+                outs.append(((r.iters, r.status, r.n_valid_opt, r.n_valid_kf, r.n_unique), r.cost,
+                             frame.T_WC.data.cpu(), kf.X_canon.cpu(), kf.C.cpu()))
+            a, b = outs
+            assert a[0] == b[0], (H, W, calib)
+            assert abs(a[1] - b[1]) <= 1e-5 * abs(a[1]), (H, W, calib)
+            np.testing.assert_allclose(a[2].numpy(), b[2].numpy(), rtol=0, atol=1e-6, err_msg=str((H, W, calib)))
+            np.testing.assert_allclose(a[3].numpy(), b[3].numpy(), rtol=1e-6, atol=1e-6, err_msg=str((H, W, calib)))
+            assert torch.equal(a[4], b[4]), (H, W, calib)
+
+
+def test_track_unique_count_after_frame_of_another_size(golden):
+    """The frame scratch (byte map, records, partials) is laid out per image size, so a workspace whose last frame had
+    another size gets its scratch re-initialised: a 48x64 frame then a 512x512 frame on the same workspace, and the
+    512x512 frame's unique-match count equals |unique(idx[valid])| computed on the host (the 48x64 frame's records
+    once left 5540 stale byte-map entries under it)."""
+    import m3s.tracker as T
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    cap = {}
+    orig = T.mast3r_match_asymmetric
+
+    def capture(*a, **k):
+        out = orig(*a, **k)
+        cap["idx"], cap["valid"] = out[0], out[1]
+        return out
+
+    T.mast3r_match_asymmetric = capture
+    try:
+        g = golden("tracking_48x64.npz")
+        kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+        FrameTracker(model, kfs, "cuda").track(frame)
+        config["use_calib"] = False
+        P = make_pair(512, 512, seed=2)
+        kf = Frame(0, (512, 512), T_WC=Sim3.Identity(1, device="cuda"))
+        kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
+        kfs = Keyframes()
+        kfs.append(kf)
+        tr = FrameTracker(SyntheticModel([P], "cuda"), kfs, "cuda")
+        tr.track(Frame(1, (512, 512), T_WC=Sim3.Identity(1, device="cuda")))
+        idx, v = cap["idx"].reshape(-1), cap["valid"].reshape(-1).bool()
+        assert tr.last_result.n_unique == int(torch.unique(idx[v]).numel())
+    finally:
+        T.mast3r_match_asymmetric = orig
