@@ -406,12 +406,10 @@ def test_track_unique_count_after_frame_of_another_size(golden):
         return out
 
     T.mast3r_match_asymmetric = capture
-    try:
-        g = golden("tracking_48x64.npz")
-        kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
-        FrameTracker(model, kfs, "cuda").track(frame)
+    P = make_pair(512, 512, seed=2)
+
+    def big():
         config["use_calib"] = False
-        P = make_pair(512, 512, seed=2)
         kf = Frame(0, (512, 512), T_WC=Sim3.Identity(1, device="cuda"))
         kf.update_pointmap(P["Xk"].cuda(), P["Ck"].cuda())
         kfs = Keyframes()
@@ -420,5 +418,12 @@ def test_track_unique_count_after_frame_of_another_size(golden):
         tr.track(Frame(1, (512, 512), T_WC=Sim3.Identity(1, device="cuda")))
         idx, v = cap["idx"].reshape(-1), cap["valid"].reshape(-1).bool()
         assert tr.last_result.n_unique == int(torch.unique(idx[v]).numel())
+
+    try:
+        big()  # the workspace grows to the 512x512 layout
+        g = golden("tracking_48x64.npz")
+        kf, frame, kfs, model = _setup(g, False, 48 * 64, 48, 64)
+        FrameTracker(model, kfs, "cuda").track(frame)  # same buffer, the 48x64 layout
+        big()
     finally:
         T.mast3r_match_asymmetric = orig
