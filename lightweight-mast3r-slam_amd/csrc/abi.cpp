@@ -19,6 +19,7 @@
 #include "m3s_ba.h"
 #include "ba_pattern.h"
 #include "m3s_track.h"
+#include "m3s_cmax.h"
 
 extern "C" {
 hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, unsigned*, hipStream_t);
@@ -224,7 +225,7 @@ static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
   w->p1 = c.take<int>((size_t)B * H * W * 2);
   w->olist = c.take<int4>((size_t)B * H * W);
   w->ocount = c.take<int>(1);
-  w->cmax = c.take<unsigned>(1);
+  w->cmax = c.take<unsigned>(M3S_CMAX_SLOTS * M3S_CMAX_STRIDE);  // m3s_cmax.h
   return c.off;
 }
 
@@ -1244,11 +1245,11 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   P.n_packed = RC ? (int)pack.size() : EL;
   P.n_dirty = 0;
   for (int k = 0; k < Kp; k++) P.n_dirty += kdirty[k];
-  // every shard edge packs (no reuse, or a first reuse plan): the pack's gathers run inside the first
-  // linearisation (ba_lin_kernel<PACK>: HBM-bound gathers under VALU-bound rows, one launch fewer);
-  // M3S_BA_FUSED_PACK=0 keeps the separate pack launch (A/B)
+  // M3S_BA_FUSED_PACK=1 (opt-in): when every shard edge packs, the pack's gathers run inside the first
+  // linearisation (ba_lin_kernel<PACK>) instead of their own launch. Measured slower at C5 (pack 4.3 ms + lin 1.9 ms
+  // -> one 8.3 ms launch: the gathers' latency at the linearisation's 3 waves per SIMD), so off by default
   const char* fpe = getenv("M3S_BA_FUSED_PACK");
-  const bool defer = P.n_packed == EL && EL > 0 && !(fpe && !strcmp(fpe, "0"));
+  const bool defer = P.n_packed == EL && EL > 0 && fpe && !strcmp(fpe, "1");
   if (defer) {
     std::lock_guard<std::mutex> lock(g_sym_mu);
     Y->pack_deferred = true;

@@ -65,8 +65,8 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
     }
 #undef T3
   }
-  if (cmax_zero != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
-    *cmax_zero = 0u;  // the refine screen's norm bound: +0.0f, raised by atomicMax in the proj launch
+  if (cmax_zero != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < M3S_CMAX_SLOTS)
+    cmax_zero[threadIdx.x * M3S_CMAX_STRIDE] = 0u;  // the refine screen's norm bound slots (m3s_cmax.h): +0.0f
   if (D11 != nullptr) {
     // f32 -> f16 of this tile's descriptor rows (B,H,W,F), 4 channels per lane-step (the per-pixel kernels'
     // layout; the refine tile path's planar layout is written by the proj launch, desc_planar below)
@@ -104,11 +104,18 @@ __device__ __forceinline__ void desc_planar(const float* __restrict__ D11, h1* _
       for (int k = 0; k < 8; k++) ss += (float)r[k] * (float)r[k];
     }
   }
-  if (cmax != nullptr) {
+  if (cmax != nullptr) {  // block max (waves through LDS), one atomic per block into its slot (m3s_cmax.h)
+    __shared__ unsigned s_max[4];
     float nmax = sqrtf(ss);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(cmax, __float_as_uint(nmax));
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = __float_as_uint(nmax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned m = s_max[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = max(m, s_max[w]);
+      atomicMax(&cmax[(blockIdx.x % M3S_CMAX_SLOTS) * M3S_CMAX_STRIDE], m);
+    }
   }
 }
 

@@ -387,7 +387,7 @@ def test_factor_schedule_stall_raises_not_silent(monkeypatch):
 def test_pack_fused_into_first_linearisation_is_bit_identical(mode, monkeypatch):
     """A call that packs every edge builds the point records inside its first linearisation (ba_lin_kernel<PACK>,
     the same pack_record values) instead of a separate ba_pack launch: poses and dx bit-identical to the separate
-    pack (M3S_BA_FUSED_PACK=0), on a 24-keyframe graph with ragged chunks."""
+    pack (the default; M3S_BA_FUSED_PACK=1 opts in), on a 24-keyframe graph with ragged chunks."""
     from m3s.synthetic import make_graph, two_way
 
     G = make_graph(n_kf=24, H=48, W=66, seed=8)
