@@ -19,15 +19,15 @@
 #include "m3s_ba.h"
 #include "ba_pattern.h"
 #include "m3s_track.h"
-#include "m3s_cmax.h"
 
 extern "C" {
-hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, unsigned*, hipStream_t);
+hipError_t m3s_launch_prep(const float*, float*, const float*, void*, int, int, int, int, int, float*, hipStream_t);
+int m3s_prep_parts(int, int, int);
 int m3s_refine_tile_ok(int, int, int, int, int, int);
 hipError_t m3s_launch_iter_proj(const float*, const float*, const float*, float*, uint8_t*, int, int, int, int, int,
                                 float, float, hipStream_t);
 hipError_t m3s_launch_proj_occlusion(const float*, const float*, const float*, const int64_t*, int*, uint8_t*, int, int,
-                                     int, int, float, float, float, int*, const float*, void*, unsigned*, hipStream_t);
+                                     int, int, float, float, float, int*, const float*, int, float*, hipStream_t);
 hipError_t m3s_launch_refine_f16(const void*, const void*, const int64_t*, int64_t*, int, int, int, int, int, int, int,
                                  hipStream_t);
 hipError_t m3s_launch_refine_f32(const float*, const float*, const int64_t*, int64_t*, int, int, int, int, int, int,
@@ -216,7 +216,8 @@ struct MatchWs {
   int* p1;        // (B,N,2) int32
   int4* olist;    // (B*N) refine deferred-outlier records
   int* ocount;    // refine deferred-outlier count
-  unsigned* cmax;  // the refine screen's descriptor-norm bound (float bits; prep zeroes, the proj launch raises)
+  float* cpart;   // the refine screen's norm bound, prep's tile partials (m3s_prep_parts)
+  float* cmax;    // ... reduced by the proj launch (refine.hip SCREEN)
 };
 
 static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
@@ -225,7 +226,8 @@ static size_t match_carve(Carver& c, int B, int H, int W, int F, MatchWs* w) {
   w->p1 = c.take<int>((size_t)B * H * W * 2);
   w->olist = c.take<int4>((size_t)B * H * W);
   w->ocount = c.take<int>(1);
-  w->cmax = c.take<unsigned>(M3S_CMAX_SLOTS * M3S_CMAX_STRIDE);  // m3s_cmax.h
+  w->cpart = c.take<float>((size_t)m3s_prep_parts(B, H, W));
+  w->cmax = c.take<float>(1);
   return c.off;
 }
 
@@ -259,16 +261,15 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   const bool screen = (screen_env == nullptr || atoi(screen_env) != 0) && planar;
   {
     Span sp("prep_rays", s);
-    // the (B,H,W,F) f16 descriptors for the per-pixel refine kernels here; the tile path's planar ones ride along
-    // with the proj launch (off the frame's dependency chain)
-    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 && !planar ? D11 : nullptr, D11h, B, H, W, F,
-                            screen ? w.cmax : nullptr, s),
+    // the f16 descriptors: the tile path's chunk planes (+ the screen's tile partials) or the (B,H,W,F) layout
+    HIP_TRY(m3s_launch_prep(X11, rays9, radius > 0 ? D11 : nullptr, D11h, B, H, W, F, planar,
+                            screen ? w.cpart : nullptr, s),
             "match prep launch");
   }
   {
     Span sp("proj_occlusion", s);
     HIP_TRY(m3s_launch_proj_occlusion(rays9, X11, X21, idx_init, p1, valid_out, B, H, W, max_iter, lambda_init,
-                                      cost_thresh, dist_thresh, w.ocount, planar ? D11 : nullptr, D11h,
+                                      cost_thresh, dist_thresh, w.ocount, w.cpart, m3s_prep_parts(B, H, W),
                                       screen ? w.cmax : nullptr, s),
             "match proj launch");
   }
@@ -277,7 +278,7 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   {
     Span sp("refine_lin", s);
     HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, w.olist,
-                                  w.ocount, screen ? reinterpret_cast<const float*>(w.cmax) : nullptr, s),
+                                  w.ocount, screen ? w.cmax : nullptr, s),
             "match refine launch");
   }
   return M3S_OK;

@@ -1,7 +1,6 @@
 // binary16 helpers shared by the refine kernels (matching.hip, refine.hip).
 #pragma once
 #include "m3s_common.hpp"
-#include "m3s_cmax.h"
 
 namespace m3s {
 

@@ -18,15 +18,38 @@ extern "C" int m3s_refine_tile_ok(int, int, int, int, int, int);
 
 namespace m3s {
 
+// Refine tile path: D11 (B,H,W,24) f32 -> f16 (RNE, == torch .half()) of pixel n into image b's three chunk planes
+// (H,W,8) (one 16-B store per plane: lanes store consecutive pixels); returns the sum of squares of its f16 values
+// (the refine screen's norm bound, refine.hip; 0 past the image)
+__device__ __forceinline__ float desc_planar(const float* __restrict__ D11, h1* __restrict__ D11h, int b, int n, int N) {
+  float ss = 0.0f;
+  if (n < N) {
+    const float4* src = reinterpret_cast<const float4*>(D11 + ((size_t)b * N + n) * 24);
+    const size_t plane = (size_t)N * 8;
+    h1* dst = D11h + (size_t)b * 3 * plane + (size_t)n * 8;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const float4 v0 = src[2 * c], v1 = src[2 * c + 1];
+      h1 r[8] = {(h1)v0.x, (h1)v0.y, (h1)v0.z, (h1)v0.w, (h1)v1.x, (h1)v1.y, (h1)v1.z, (h1)v1.w};
+      *reinterpret_cast<uint4*>(dst + c * plane) = *reinterpret_cast<uint4*>(r);
+#pragma unroll
+      for (int k = 0; k < 8; k++) ss += (float)r[k] * (float)r[k];
+    }
+  }
+  return ss;
+}
+
 // ------------------------------------------------------------------------------------------
 // prep: rays = X/max(|X|,1e-12); gx, gy = Scharr/32 with reflect padding; out (B,H,W,9).
 // One 16x16 tile per 256-thread block, normalised rays of an 18x18 halo staged in LDS.
-// Also converts D11 (B,H,W,F) f32 -> f16 (RNE, == torch .half()) for the same pixels.
+// Also converts D11 (B,H,W,F) f32 -> f16 (RNE, == torch .half()) for the same pixels: planar (refine tile path, one
+// pixel per thread) with the tile's descriptor-norm partial max |D11h[pixel]|_2 into cnorm_part (nullable), else in
+// the (B,H,W,F) layout of the per-pixel refine kernels.
 // ------------------------------------------------------------------------------------------
 #define PREP_T 16
 __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict__ X11, float* __restrict__ rays9,
                                                         const float* __restrict__ D11, h1* __restrict__ D11h, int H,
-                                                        int W, int F, unsigned* __restrict__ cmax_zero) {
+                                                        int W, int F, int planar, float* __restrict__ cnorm_part) {
   __shared__ float tile[(PREP_T + 2) * (PREP_T + 2) * 3];
   const int b = blockIdx.z;
   const int u0 = blockIdx.x * PREP_T, v0 = blockIdx.y * PREP_T;
@@ -65,9 +88,22 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
     }
 #undef T3
   }
-  if (cmax_zero != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < M3S_CMAX_SLOTS)
-    cmax_zero[threadIdx.x * M3S_CMAX_STRIDE] = 0u;  // the refine screen's norm bound slots (m3s_cmax.h): +0.0f
-  if (D11 != nullptr) {
+  if (D11 != nullptr && planar) {
+    const float ss = desc_planar(D11, D11h, b, (x < W && y < H) ? y * W + x : H * W, H * W);
+    if (cnorm_part != nullptr) {
+      // the tile's max |D11h[pixel]|_2, one partial per block (proj_occlusion reduces them before refine reads the
+      // bound); NaN / inf descriptors give a NaN / inf partial, which switches the screen off for every lane
+      __shared__ float s_max[4];
+      float nmax = sqrtf(ss);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
+      if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = nmax;
+      __syncthreads();
+      if (threadIdx.x == 0)
+        cnorm_part[((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
+            fmaxf_nan(fmaxf_nan(s_max[0], s_max[1]), fmaxf_nan(s_max[2], s_max[3]));
+    }
+  } else if (D11 != nullptr) {
     // f32 -> f16 of this tile's descriptor rows (B,H,W,F), 4 channels per lane-step (the per-pixel kernels'
     // layout; the refine tile path's planar layout is written by the proj launch, desc_planar below)
     for (int t = threadIdx.x; t < PREP_T * PREP_T * (F / 4); t += blockDim.x) {
@@ -83,40 +119,15 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
   }
 }
 
-// Refine tile path: D11 (B,H,W,24) f32 -> f16 (RNE, == torch .half()) into image b's three chunk planes (H,W,8), one
-// pixel per thread (one 16-B store per plane: lanes store consecutive pixels), and the refine screen's bound
-// max |D11h[pixel]|_2 (refine.hip) raised by one atomicMax per wave on the float's bits (non-negative: ordered as
-// unsigned; a NaN has the largest bits and wins, which switches the screen off for every lane). Run by extra blocks
-// of the proj_occlusion launch: HBM-bound conversion beside the latency-bound LM search, off the frame's chain.
-__device__ __forceinline__ void desc_planar(const float* __restrict__ D11, h1* __restrict__ D11h, int b, int n, int N,
-                                            unsigned* __restrict__ cmax) {
-  float ss = 0.0f;
-  if (n < N) {
-    const float4* src = reinterpret_cast<const float4*>(D11 + ((size_t)b * N + n) * 24);
-    const size_t plane = (size_t)N * 8;
-    h1* dst = D11h + (size_t)b * 3 * plane + (size_t)n * 8;
+// max of the prep partials into cmax[0] (the refine screen's descriptor-norm bound), by the first wave of one block
+// of the launch between prep and refine (proj_occlusion)
+__device__ __forceinline__ void reduce_cnorm(const float* __restrict__ part, int nparts, float* __restrict__ cmax) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.0f;
+  for (int i = lane; i < nparts; i += 64) m = fmaxf_nan(m, part[i]);
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-      const float4 v0 = src[2 * c], v1 = src[2 * c + 1];
-      h1 r[8] = {(h1)v0.x, (h1)v0.y, (h1)v0.z, (h1)v0.w, (h1)v1.x, (h1)v1.y, (h1)v1.z, (h1)v1.w};
-      *reinterpret_cast<uint4*>(dst + c * plane) = *reinterpret_cast<uint4*>(r);
-#pragma unroll
-      for (int k = 0; k < 8; k++) ss += (float)r[k] * (float)r[k];
-    }
-  }
-  if (cmax != nullptr) {  // block max (waves through LDS), one atomic per block into its slot (m3s_cmax.h)
-    __shared__ unsigned s_max[4];
-    float nmax = sqrtf(ss);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) nmax = fmaxf_nan(nmax, __shfl_xor(nmax, off, 64));
-    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = __float_as_uint(nmax);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned m = s_max[0];
-      for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = max(m, s_max[w]);
-      atomicMax(&cmax[(blockIdx.x % M3S_CMAX_SLOTS) * M3S_CMAX_STRIDE], m);
-    }
-  }
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf_nan(m, __shfl_xor(m, off, 64));
+  if (lane == 0) *cmax = m;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -235,20 +246,11 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
     const float* __restrict__ rays, const float* __restrict__ X11, const float* __restrict__ X21,
     const int64_t* __restrict__ idx_init, int* __restrict__ p1, uint8_t* __restrict__ valid, int H, int W,
     int max_iter, float lambda_init, float cost_thresh, float dist_thresh, int* zero_counter,
-    const float* __restrict__ D11, h1* __restrict__ D11h, unsigned* __restrict__ cmax) {
+    const float* __restrict__ cnorm_part, int nparts, float* __restrict__ cmax) {
   const int N = H * W;
-  // with D11: odd blocks convert the descriptors (desc_planar), even blocks run the LM search
-  int bx = blockIdx.x, nbx = gridDim.x;
-  if (D11 != nullptr) {
-    if (bx & 1) {
-      desc_planar(D11, D11h, blockIdx.y, (bx >> 1) * blockDim.x + threadIdx.x, N, cmax);
-      return;
-    }
-    bx >>= 1;
-    nbx = (nbx + 1) >> 1;
-  }
+  if (cmax != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) reduce_cnorm(cnorm_part, nparts, cmax);
   // contiguous pixel runs per XCD: each XCD's L2 then holds the rays rows its LM gathers touch
-  const int n = xcd_remap(bx, nbx) * blockDim.x + threadIdx.x;
+  const int n = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (zero_counter != nullptr && n == 0 && b == 0) *zero_counter = 0;  // refine's outlier list (next launch)
   if (n >= N) return;
@@ -404,15 +406,18 @@ __global__ void __launch_bounds__(256) refine_f32_kernel(const float* __restrict
 // ------------------------------------------------------------------------------------------
 // launchers (called from abi.cpp)
 // ------------------------------------------------------------------------------------------
-// D11 (nullable): convert the descriptors here in the (B,H,W,F) layout (per-pixel refine kernels); the planar
-// layout of the refine tile path is converted by the proj launch instead. cmax_zero (nullable): reset the screen's
-// norm bound for this call.
+// D11 (nullable): convert the descriptors too, planar (refine tile path, F = 24; cnorm_part nullable: the tile
+// partials of the screen's norm bound, B * tiles floats) or in the (B,H,W,F) layout (per-pixel refine kernels)
 extern "C" hipError_t m3s_launch_prep(const float* X11, float* rays9, const float* D11, void* D11h, int B, int H,
-                                      int W, int F, unsigned* cmax_zero, hipStream_t s) {
+                                      int W, int F, int planar, float* cnorm_part, hipStream_t s) {
   dim3 grid((W + PREP_T - 1) / PREP_T, (H + PREP_T - 1) / PREP_T, B);
   hipLaunchKernelGGL(m3s::prep_rays_kernel, grid, dim3(256), 0, s, X11, rays9, D11,
-                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, cmax_zero);
+                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, planar, cnorm_part);
   return hipGetLastError();
+}
+
+extern "C" int m3s_prep_parts(int B, int H, int W) {
+  return B * ((W + PREP_T - 1) / PREP_T) * ((H + PREP_T - 1) / PREP_T);
 }
 
 extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
@@ -427,13 +432,12 @@ extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, 
 extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* X11, const float* X21,
                                                 const int64_t* idx_init, int* p1, uint8_t* valid, int B, int H, int W,
                                                 int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-                                                int* zero_counter, const float* D11, void* D11h, unsigned* cmax,
+                                                int* zero_counter, const float* cnorm_part, int nparts, float* cmax,
                                                 hipStream_t s) {
-  // D11 (nullable, F = 24): the planar conversion for the refine tile path rides along (odd blocks; desc_planar)
-  dim3 grid((H * W + 255) / 256 * (D11 != nullptr ? 2 : 1), B);
+  // cmax (nullable): one wave reduces prep's tile partials into the refine screen's bound
+  dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
-                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter, D11,
-                     reinterpret_cast<m3s::h1*>(D11h), cmax);
+                     max_iter, lambda_init, cost_thresh, dist_thresh, zero_counter, cnorm_part, nparts, cmax);
   return hipGetLastError();
 }
 

@@ -643,12 +643,7 @@ __global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restric
     float qq = 0.0f;
 #pragma unroll
     for (int k = 0; k < F / 2; k++) qq = __builtin_amdgcn_fdot2(q[k], q[k], qq, false);
-    // the bound's slots (m3s_cmax.h), max-reduced as unsigned bits (a NaN's bits are the largest: it wins)
-    const unsigned* cs = reinterpret_cast<const unsigned*>(cmaxp);
-    unsigned cb = cs[(t.lane % M3S_CMAX_SLOTS) * M3S_CMAX_STRIDE];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cb = max(cb, (unsigned)__shfl_xor((int)cb, off, 64));
-    const float pq = sqrtf(qq) * __uint_as_float(cb) * 1.001f;  // |q|_2 |c|_2 bound, rounded up
+    const float pq = sqrtf(qq) * *cmaxp * 1.001f;  // |q|_2 |c|_2 bound, rounded up
     t.sok = pq <= 16384.0f;                         // false for NaN / inf
     t.bq = t.sok ? 0.0125f * pq + 0x1p-18f : 0.0f;
   }
