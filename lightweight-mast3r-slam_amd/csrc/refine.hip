@@ -138,17 +138,24 @@ __device__ __forceinline__ void screen_chunk(const uint4* base, const h2* q4, fl
   constexpr int G = 7;
 #pragma unroll
   for (int i = 0; i < G; i++) {
-    // the column's 7 candidate reads in flight together (one LDS latency per column, not per candidate)
-    uint4 c[G];
+    // the column's candidate reads in flight together (RT_COLBATCH of them: one LDS latency per batch, not per
+    // candidate)
+#ifndef RT_COLBATCH
+#define RT_COLBATCH 7
+#endif
 #pragma unroll
-    for (int j = 0; j < G; j++) c[j] = base[j * D * STRIDE + i * D];
+    for (int j0 = 0; j0 < G; j0 += RT_COLBATCH) {
+      uint4 c[RT_COLBATCH];
 #pragma unroll
-    for (int j = 0; j < G; j++) {
-      const h2* cv = reinterpret_cast<const h2*>(&c[j]);
-      float t = a[i * G + j];
+      for (int j = j0; j < min(G, j0 + RT_COLBATCH); j++) c[j - j0] = base[j * D * STRIDE + i * D];
 #pragma unroll
-      for (int k = 0; k < 4; k++) t = __builtin_amdgcn_fdot2(q4[k], cv[k], t, false);
-      a[i * G + j] = t;
+      for (int j = j0; j < min(G, j0 + RT_COLBATCH); j++) {
+        const h2* cv = reinterpret_cast<const h2*>(&c[j - j0]);
+        float t = a[i * G + j];
+#pragma unroll
+        for (int k = 0; k < 4; k++) t = __builtin_amdgcn_fdot2(q4[k], cv[k], t, false);
+        a[i * G + j] = t;
+      }
     }
     // pin the column's dot products here: otherwise the last chunk's are sunk into the survivor code and all 49
     // candidate loads stay live across it (1000+ spilled VGPRs)
@@ -573,8 +580,11 @@ __device__ __forceinline__ void store_out(void* outv, size_t bn, int W, int cu, 
 // P1_I64: p1 given as (B,N,2) int64 (reference op) else int32 (fused); LIN_OUT: write idx = u + W v.
 // SCREEN: bound-screened scoring (cmaxp = the descriptor-norm bound written by prep / proj_occlusion).
 // LIN_OUT (fused path) reads the PLANAR D11h of prep_rays_kernel.
+#ifndef RT_MIN_BLOCKS  // blocks per CU the register budget is sized for (4: 128 VGPRs, the LDS limit too)
+#define RT_MIN_BLOCKS 4
+#endif
 template <bool D21_F32, bool P1_I64, bool LIN_OUT, bool SCREEN>
-__global__ void __launch_bounds__(256, 4) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
+__global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
                                                              const void* __restrict__ p1v, void* __restrict__ outv,
                                                              int H, int W, int dilation_max, int tiles_x,
                                                              int tiles_per_img, int nblocks, int4* olist,
