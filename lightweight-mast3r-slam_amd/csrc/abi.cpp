@@ -277,7 +277,11 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   // (matching.py:78-88); D11h is never read then.
   {
     Span sp("refine_lin", s);
-    HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0, w.olist,
+    // M3S_REFINE_INPLACE=1 (experiment): no deferred-pixel list, each wave scores its window outliers in place
+    const char* inplace_env = getenv("M3S_REFINE_INPLACE");
+    const bool inplace = inplace_env != nullptr && inplace_env[0] == '1';
+    HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0,
+                                  inplace ? nullptr : w.olist,
                                   w.ocount, screen ? w.cmax : nullptr, s),
             "match refine launch");
   }
