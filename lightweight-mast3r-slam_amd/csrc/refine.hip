@@ -49,6 +49,9 @@ namespace m3s {
 // while chunk c is screened (the d = 2 cover is 23 x 45-47 on 97.6 % of the synthetic 512x512 tiles)
 #define RT_DROWS 26
 #define RT_DBUF (RT_DROWS * RT_PCOLS)
+#ifndef RT_INPLACE_MAX  // window outliers a wave scores in place at one level (more: deferred to the list)
+#define RT_INPLACE_MAX 8
+#endif
 
 typedef __attribute__((address_space(1))) const void* gvoid_t;
 typedef __attribute__((address_space(3))) void* lvoid_t;
@@ -338,7 +341,10 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   }
 #endif
   if (om) {
-    if (t.olist != nullptr) {
+    // a wave with a few window outliers scores them in place (one wave-level each, while the rest of the tile waits
+    // at the next barrier); more than RT_INPLACE_MAX go to the deferred list (one wave per pixel in
+    // refine_outlier_kernel), which keeps pathological inputs (scattered warm starts: every lane an outlier) parallel
+    if (t.olist != nullptr && __popcll(om) > RT_INPLACE_MAX) {
       // defer: one atomic per wave reserves the slots, lanes write {pixel, centre, max bits, level}
       const int leader = __ffsll((long long)om) - 1;
       int base = 0;

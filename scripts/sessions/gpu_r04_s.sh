@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 4: refine window outliers scored in place by their wave (M3S_REFINE_INPLACE=1: no deferred list, no outlier
+# round 4: refine window outliers: hybrid (default: in place up to RT_INPLACE_MAX per wave, else deferred) vs
+# pure in place (M3S_REFINE_INPLACE=1: no deferred list, no outlier
 # launch) vs the deferred list + refine_outlier_kernel; idx checksum must match; then the tracking bench A/B
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -13,7 +14,7 @@ for r in 1 2; do
 done
 } 2>&1 | grep -v amdgpu.ids > gpurun_out/r04s_refine_exp.txt
 cat gpurun_out/r04s_refine_exp.txt
-M3S_REFINE_INPLACE=1 timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_matching.py tests/test_gpu_refine_screen.py > gpurun_out/r04s_pytest.txt 2>&1
+timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_matching.py tests/test_gpu_refine_screen.py > gpurun_out/r04s_pytest.txt 2>&1
 rc=$?; tail -3 gpurun_out/r04s_pytest.txt; [ $rc -eq 0 ] || exit $rc
 A="--steps 100 --warmup 10 --no-ba --no-cpu --no-retrieval --no-store --no-peaks"
 for r in 1 2; do
