@@ -80,11 +80,9 @@ __device__ __forceinline__ void load_chunks(const h1* p, size_t N, uint4& c0, ui
   c2 = *reinterpret_cast<const uint4*>(p + 2 * cs);
 }
 
-// pend (wave-uniform): max_score is not known yet (the bound-screened tile took the previous level's winner without
-// its exact score, refine_level): it is the exact score of the centre candidate (3,3), scored here by lane 24.
 template <int D, bool PLANAR>
 __device__ __forceinline__ void wave_level(const h1* __restrict__ img, int H, int W, const h2* sq, int& cu, int& cv,
-                                           h1& max_score, int lane, bool pend = false) {
+                                           h1& max_score, int lane) {
   constexpr int R = 3, RD = R * D, G = 2 * R + 1;
   const int ci = lane / G, cj = lane % G;
   const int u = cu - RD + ci * D, v = cv - RD + cj * D;
@@ -96,11 +94,6 @@ __device__ __forceinline__ void wave_level(const h1* __restrict__ img, int H, in
   add8(sc, &sq[0], c0);
   add8(sc, &sq[4], c1);
   add8(sc, &sq[8], c2);
-  if (pend) {
-    const int b = __shfl((int)*reinterpret_cast<const unsigned short*>(&sc), G * G / 2, 64);
-    const unsigned short bs = (unsigned short)b;
-    max_score = *reinterpret_cast<const h1*>(&bs);
-  }
   const float sf = (ok && sc == sc) ? (float)sc : -INFINITY;  // NaN never wins a strict '>'
   float vmax = sf;
 #pragma unroll
@@ -290,7 +283,7 @@ struct TileCtx {
 
 template <int D, bool SCREEN, bool PLANAR>
 __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, const h2* q, int& cu, int& cv,
-                                             h1& max_score, bool& pend, uint4* lds, int (*s_red)[4], bool first) {
+                                             h1& max_score, uint4* lds, int (*s_red)[4], bool first) {
   constexpr int R = 3, G = 2 * R + 1, F = 24, RD = R * D;
   const int lane = t.lane, wid = t.wid, H = t.H, W = t.W;
   // bbox of the inlier centres (within 16 px of pixel + the tile's flow estimate t.fu/t.fv)
@@ -360,7 +353,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       if (outl) {
         const int rank = __popcll(om & ((1ull << lane) - 1ull));
         const unsigned short mb = *reinterpret_cast<const unsigned short*>(&max_score);
-        t.olist[base + rank] = make_int4(t.bn, (cu & 0xffff) | (cv << 16), (int)mb | (D << 16), pend ? 1 : 0);
+        t.olist[base + rank] = make_int4(t.bn, (cu & 0xffff) | (cv << 16), (int)mb | (D << 16), 0);
         active = false;
       }
     } else {
@@ -379,12 +372,11 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
           const int v = __shfl(*reinterpret_cast<const int*>(&q[k]), src, 64);
           sq[k] = *reinterpret_cast<const h2*>(&v);
         }
-        wave_level<D, PLANAR>(t.img, H, W, sq, scu, scv, smax, lane, __shfl((int)pend, src, 64) != 0);
+        wave_level<D, PLANAR>(t.img, H, W, sq, scu, scv, smax, lane);
         if (lane == src) {
           cu = scu;
           cv = scv;
           max_score = smax;
-          pend = false;
         }
       }
     }
@@ -396,13 +388,6 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     float a[G * G];
 #pragma unroll
     for (int c = 0; c < G * G; c++) a[c] = 0.0f;
-    // pend: the running max is the previous level's winner's exact score, still to be computed: that winner is this
-    // level's centre candidate (3,3), whose exact chain is summed from the window chunk by chunk
-    const bool need_c = __ballot(lane_in && pend) != 0;
-    h1 cs = (h1)0.0f;
-    auto centre = [&](const uint4* base, int chunk, int stride) {
-      if (need_c && lane_in && pend) add8(cs, &q[chunk * 4], base[3 * D * stride + 3 * D]);
-    };
     __syncthreads();  // the reduction scratch aliases the window: its readers are done
     if (packed) {  // (d = 1 only) the three chunk planes in one fill
 #ifndef RT_NOLOAD
@@ -423,9 +408,6 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
         screen_chunk<D, RT_PCOLS>(&lds[b0], &q[0], a);
         screen_chunk<D, RT_PCOLS>(&lds[RT_PPLANE + b0], &q[4], a);
         screen_chunk<D, RT_PCOLS>(&lds[2 * RT_PPLANE + b0], &q[8], a);
-        centre(&lds[b0], 0, RT_PCOLS);
-        centre(&lds[RT_PPLANE + b0], 1, RT_PCOLS);
-        centre(&lds[2 * RT_PPLANE + b0], 2, RT_PCOLS);
       }
 #endif
     } else if (dbuf) {  // (d = 2 only) chunk c + 1 lands in the other buffer while chunk c is screened
@@ -449,20 +431,17 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       fill(1, RT_DBUF);
 #ifndef RT_NOCOMP
       if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[b0], &q[0], a);
-      centre(&lds[b0], 0, RT_PCOLS);
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // chunk 1 landed; every wave is done with buffer 0
       fill(2, 0);
 #ifndef RT_NOCOMP
       if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[RT_DBUF + b0], &q[4], a);
-      centre(&lds[RT_DBUF + b0], 1, RT_PCOLS);
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 #ifndef RT_NOCOMP
       if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[b0], &q[8], a);
-      centre(&lds[b0], 2, RT_PCOLS);
 #endif
     } else {
 #pragma unroll
@@ -480,13 +459,8 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
         __syncthreads();
 #ifndef RT_NOCOMP
         if (lane_in) screen_chunk<D>(&lds[by * RT_COLS + bx], &q[chunk * 4], a);
-        centre(&lds[by * RT_COLS + bx], chunk, RT_COLS);
 #endif
       }
-    }
-    if (lane_in && pend) {
-      max_score = cs;
-      pend = false;
     }
     if (lane_in) {
       uint64_t vm = (1ull << (G * G)) - 1ull;  // in-image candidates
@@ -527,16 +501,6 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       m = 0;
 #endif
       int bi = -1;
-      // a sole survivor whose screen score exceeds the running max by the bound (so S_half > max_score whatever the
-      // rounding) is the level's screen maximum (the centre's S_dot2 is <= max_score + B), hence the only candidate
-      // that can beat the running max: the level's winner, taken without its exact chain. Its exact score is needed
-      // only as the next level's running max, where it is the centre candidate, scored from that level's window
-      // (pend; by wave_level for a lane that leaves the window)
-      if (t.sok && __popcll(m) == 1 && lmax > (float)max_score + t.bq) {
-        bi = __ffsll((long long)m) - 1;
-        m = 0;
-        pend = true;
-      }
       if (packed)
         exact_survivors_lds<D>(&lds[by * RT_PCOLS + bx], q, m, max_score, bi);
       else
@@ -704,18 +668,17 @@ __global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h
   if (threadIdx.x == 0 && blockIdx.x < 8192) g_refine_bstamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
   h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
-  bool pend = false;         // max_score not computed yet (refine_level: a sole sure winner)
   for (int d = dilation_max; d > 0; d--) {
     const bool first = d == dilation_max;
     switch (d) {
-      case 8: refine_level<8, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 7: refine_level<7, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 6: refine_level<6, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 5: refine_level<5, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 4: refine_level<4, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 3: refine_level<3, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      case 2: refine_level<2, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
-      default: refine_level<1, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, pend, lds, s_red, first); break;
+      case 8: refine_level<8, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 7: refine_level<7, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 6: refine_level<6, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 5: refine_level<5, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 4: refine_level<4, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 3: refine_level<3, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      case 2: refine_level<2, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
+      default: refine_level<1, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
     }
   }
   if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
@@ -756,22 +719,20 @@ __global__ void __launch_bounds__(256) refine_outlier_kernel(const h1* __restric
     const unsigned short mb = (unsigned short)(r.z & 0xffff);
     h1 max_score = *reinterpret_cast<const h1*>(&mb);
     const int d0 = r.z >> 16;
-    bool pend = r.w != 0;  // the tile took the previous level's winner without its exact score
     const h1* img = D11h + (bn / N) * (size_t)N * F;
     h2 q[F / 2];
     load_query<F, D21_F32>(D21, bn, q);
     for (int d = d0; d > 0; d--) {
       switch (d) {
-        case 8: wave_level<8, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 7: wave_level<7, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 6: wave_level<6, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 5: wave_level<5, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 4: wave_level<4, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 3: wave_level<3, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        case 2: wave_level<2, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
-        default: wave_level<1, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane, pend); break;
+        case 8: wave_level<8, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 7: wave_level<7, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 6: wave_level<6, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 5: wave_level<5, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 4: wave_level<4, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 3: wave_level<3, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        case 2: wave_level<2, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
+        default: wave_level<1, LIN_OUT>(img, H, W, q, cu, cv, max_score, lane); break;
       }
-      pend = false;
     }
     if (lane == 0) store_out<LIN_OUT>(outv, bn, W, cu, cv);
   }
