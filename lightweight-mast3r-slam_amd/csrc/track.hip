@@ -324,6 +324,9 @@ typedef __attribute__((address_space(1))) unsigned long long gull;
 #define GN_THREADS 256  // threads of a GN block (one block per CU)
 #endif
 #define GN_PPT (1024 / GN_THREADS)  // points per thread per round (1024 per block): record loads issued before any math
+#ifndef GN_PAIR  // points in float2 pairs, fp32 product sums per thread (gn_pair) instead of fp64 FMAs per product
+#define GN_PAIR 1
+#endif
 #define GN_MAX_BLOCKS 256           // partial rows per iteration slot
 
 // ---- the 36 fp64 sums of a wave, reduce-scattered over its lanes (deterministic, no LDS) ----
@@ -464,6 +467,131 @@ __device__ __forceinline__ void gn_point(const TrackParams& p, const float* T, f
 //      system, retracts and tests convergence itself: the same instructions on the same bytes, so every block
 //      holds the same T bit for bit, and no broadcast hop or serial last-block tail sits on the chain.
 // Spins are bounded: a stalled hand-off ends the frame with status STALLED (the host raises), never a hang.
+// ---- two points per lane (float2 lanes), GN_PAIR builds: every per-point operation of gn_point, elementwise on
+// the pair (so each point's rounding is gn_point's), with the row products accumulated in fp32 (packed FMAs, one
+// rounding per product-sum) over the thread's points and added to the fp64 sums once per iteration (gn_flush):
+// half the instructions of the fp64 product-sums at the GN launch's one wave per SIMD ----
+typedef float gf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gf2 g2sqrt(gf2 x) { return gf2{sqrtf(x.x), sqrtf(x.y)}; }
+__device__ __forceinline__ gf2 g2fma(gf2 a, gf2 b, gf2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <unsigned MASK = 0x7fu>
+__device__ __forceinline__ void acc_row2(gf2* acc, const gf2 J[7], gf2 r, gf2 si, float k) {
+  const gf2 wr = si * r;
+  const gf2 ra = {fabsf(wr.x), fabsf(wr.y)};
+  const gf2 hub = {ra.x < k ? 1.0f : k / ra.x, ra.y < k ? 1.0f : k / ra.y};
+  const gf2 rob = si * g2sqrt(hub);
+  gf2 A[7];
+#pragma unroll
+  for (int c = 0; c < 7; c++) A[c] = rob * J[c];
+  const gf2 b = rob * r;
+  int l = 0;
+#pragma unroll
+  for (int c = 0; c < 7; c++) {
+#pragma unroll
+    for (int d = c; d < 7; d++) {
+      if ((MASK >> c) & (MASK >> d) & 1u) acc[l] = g2fma(A[c], A[d], acc[l]);
+      l++;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 7; c++)
+    if ((MASK >> c) & 1u) acc[28 + c] = g2fma(-A[c], b, acc[28 + c]);  // g = -A^T b
+  acc[35] = g2fma(0.5f * b, b, acc[35]);
+}
+
+__device__ __forceinline__ void chain_row2(const gf2 dh[3], const gf2 Y[3], gf2 J[7]) {
+  J[0] = -dh[0];
+  J[1] = -dh[1];
+  J[2] = -dh[2];
+  J[3] = -(dh[1] * -Y[2] + dh[2] * Y[1]);
+  J[4] = -(dh[0] * Y[2] + dh[2] * -Y[0]);
+  J[5] = -(dh[0] * -Y[1] + dh[1] * Y[0]);
+  J[6] = -(dh[0] * Y[0] + dh[1] * Y[1] + dh[2] * Y[2]);
+}
+
+__device__ __forceinline__ void actSim3_2(const float* T, const gf2 X[3], gf2 Y[3]) {
+  const float* q = &T[3];
+  const gf2 uv0 = 2.0f * (q[1] * X[2] - q[2] * X[1]);
+  const gf2 uv1 = 2.0f * (q[2] * X[0] - q[0] * X[2]);
+  const gf2 uv2 = 2.0f * (q[0] * X[1] - q[1] * X[0]);
+  const gf2 y0 = X[0] + q[3] * uv0 + (q[1] * uv2 - q[2] * uv1);
+  const gf2 y1 = X[1] + q[3] * uv1 + (q[2] * uv0 - q[0] * uv2);
+  const gf2 y2 = X[2] + q[3] * uv2 + (q[0] * uv1 - q[1] * uv0);
+  Y[0] = y0 * T[7] + T[0];
+  Y[1] = y1 * T[7] + T[1];
+  Y[2] = y2 * T[7] + T[2];
+}
+
+// points a and b (b = a with weight 0 when the thread has no second point: exact zeros unless a's own row is
+// non-finite, which poisons the sums anyway)
+__device__ __forceinline__ void gn_pair(const TrackParams& p, const float* T, float4 a0, float4 a1, float4 b0,
+                                        float4 b1, gf2* acc) {
+  const gf2 X[3] = {gf2{a0.x, b0.x}, gf2{a0.y, b0.y}, gf2{a0.z, b0.z}};
+  gf2 Y[3];
+  actSim3_2(T, X, Y);
+  const gf2 sq = {a1.w, b1.w};
+  if (p.mode == 0) {
+    const gf2 d = g2sqrt(Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2]);
+    const gf2 di = 1.0f / d;
+    const gf2 di2 = di * di;
+    const gf2 rr[3] = {di * Y[0], di * Y[1], di * Y[2]};
+    const gf2 res[4] = {gf2{a0.w, b0.w} - rr[0], gf2{a1.x, b1.x} - rr[1], gf2{a1.y, b1.y} - rr[2],
+                        gf2{a1.z, b1.z} - d};
+    const gf2 si_r = p.c_a * sq, si_d = p.c_b * sq;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      gf2 dh[3];
+#pragma unroll
+      for (int m = 0; m < 3; m++) dh[m] = di * ((k == m ? 1.0f : 0.0f) - di2 * (Y[k] * Y[m]));
+      gf2 J[7];
+      chain_row2(dh, Y, J);
+      acc_row2(acc, J, res[k], si_r, p.huber_k);
+    }
+    gf2 J[7];
+    chain_row2(rr, Y, J);
+    acc_row2(acc, J, res[3], si_d, p.huber_k);
+  } else {
+    const gf2 x = Y[0], y = Y[1], z = Y[2];
+    const gf2 pu = p.K[0] * x + p.K[1] * y + p.K[2] * z;
+    const gf2 pv = p.K[3] * x + p.K[4] * y + p.K[5] * z;
+    const gf2 pw = p.K[6] * x + p.K[7] * y + p.K[8] * z;
+    const gf2 u = pu / pw, v = pv / pw;
+    const bool vz0 = z.x > p.depth_eps, vz1 = z.y > p.depth_eps;
+    const gf2 logz = {vz0 ? logf(z.x) : 0.0f, vz1 ? logf(z.y) : 0.0f};
+    const float ub = p.pixel_border, uh = (float)(p.W - 1) - p.pixel_border, vh = (float)(p.H - 1) - p.pixel_border;
+    const bool ok0 = (u.x > ub) && (u.x < uh) && (v.x > ub) && (v.x < vh) && vz0 && (a1.z != 0.0f);
+    const bool ok1 = (u.y > ub) && (u.y < uh) && (v.y > ub) && (v.y < vh) && vz1 && (b1.z != 0.0f);
+    const gf2 vf = {ok0 ? 1.0f : 0.0f, ok1 ? 1.0f : 0.0f};
+    const gf2 si_p = vf * (p.c_a * sq), si_z = vf * (p.c_b * sq);
+    const gf2 zi = 1.0f / z;
+    const gf2 res[3] = {gf2{a0.w, b0.w} - u, gf2{a1.x, b1.x} - v, gf2{a1.y, b1.y} - logz};
+    const gf2 z2 = {0.0f, 0.0f};
+    gf2 dh[3], J[7];
+    dh[0] = p.K[0] * zi;
+    dh[1] = z2;
+    dh[2] = (-p.K[0] * x * zi) * zi;
+    chain_row2(dh, Y, J);
+    acc_row2<0b1111101u>(acc, J, res[0], si_p, p.huber_k);
+    dh[0] = z2;
+    dh[1] = p.K[4] * zi;
+    dh[2] = (-p.K[4] * y * zi) * zi;
+    chain_row2(dh, Y, J);
+    acc_row2<0b1111110u>(acc, J, res[1], si_p, p.huber_k);
+    dh[0] = z2;
+    dh[1] = z2;
+    dh[2] = zi;
+    chain_row2(dh, Y, J);
+    acc_row2<0b1011100u>(acc, J, res[2], si_z, p.huber_k);
+  }
+}
+
+// the thread's fp32 pair sums into its fp64 sums
+__device__ __forceinline__ void gn_flush(double* acc, const gf2* a2) {
+#pragma unroll
+  for (int c = 0; c < GN_NSUM; c++) acc[c] += (double)a2[c].x + (double)a2[c].y;
+}
+
 //
 // SETUP (folded setup, M3S_TRACK_FOLD_SETUP=1): no track_setup launch. Every block derives the initial T_CkCf
 // itself (track_state_init's arithmetic), builds its points' records in the first iteration (setup_point: the
@@ -552,9 +680,27 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     double acc[GN_NSUM];
 #pragma unroll
     for (int c = 0; c < GN_NSUM; c++) acc[c] = 0.0;
+#if GN_PAIR
+    gf2 a2[GN_NSUM];
+#pragma unroll
+    for (int c = 0; c < GN_NSUM; c++) a2[c] = gf2{0.0f, 0.0f};
+    auto pair = [&](int na, const float4& xa0, const float4& xa1, const float4& xb0, const float4& xb1) {
+      if (na >= p.N) return;
+      if (na + stride < p.N) {
+        gn_pair(p, T, xa0, xa1, xb0, xb1, a2);
+      } else {  // no second point: the first again with weight 0
+        float4 z1 = xa1;
+        z1.w = 0.0f;
+        gn_pair(p, T, xa0, xa1, xa0, z1, a2);
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < GN_PPT; u += 2) pair(n00 + u * stride, c0[u], c1[u], c0[u + 1], c1[u + 1]);
+#else
 #pragma unroll
     for (int u = 0; u < GN_PPT; u++)
       if (n00 + u * stride < p.N) gn_point(p, T, c0[u], c1[u], acc);
+#endif
     for (int n0 = n00 + GN_PPT * stride; n0 < p.N; n0 += GN_PPT * stride) {
       float4 r0[GN_PPT], r1[GN_PPT];
 #pragma unroll
@@ -576,10 +722,18 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
           r1[u] = rec[2 * (size_t)n + 1];
         }
       }
+#if GN_PAIR
+#pragma unroll
+      for (int u = 0; u < GN_PPT; u += 2) pair(n0 + u * stride, r0[u], r1[u], r0[u + 1], r1[u + 1]);
+#else
 #pragma unroll
       for (int u = 0; u < GN_PPT; u++)
         if (n0 + u * stride < p.N) gn_point(p, T, r0[u], r1[u], acc);
+#endif
     }
+#if GN_PAIR
+    gn_flush(acc, a2);
+#endif
     GN_STAMP(1);
     s_w[wid][lane] = wave_sum36(acc, lane);
     if (SETUP && it == 0) {  // the wave's valid counts, packed (n_valid_kf << 32) | n_valid_opt like track_setup's
