@@ -462,9 +462,10 @@ extern "C" int m3s_track(const m3s_track_inputs* in, const m3s_track_config* cfg
     g_track_clean.erase(workspace);  // dirty until this call has published
   }
   if (!clean) HIP_TRY(m3s_launch_track_init(&a, in->T_WCf, in->T_WCk, N, s), "track init launch");
-  // M3S_TRACK_FOLD_SETUP=1: the per-point setup runs inside the GN launch's first iteration (no track_setup launch)
+  // the per-point setup runs inside the GN launch's first iteration (gn_loop_kernel<true>: no track_setup launch);
+  // M3S_TRACK_FOLD_SETUP=0 keeps the separate track_setup launch (A/B)
   const char* fold_env = getenv("M3S_TRACK_FOLD_SETUP");
-  const int fold = fold_env != nullptr && fold_env[0] == '1';
+  const int fold = !(fold_env != nullptr && fold_env[0] == '0');
   if (!fold) {
     Span sp("track_setup", s);
     HIP_TRY(m3s_launch_track_setup(&a, &p, s), "track setup launch");
