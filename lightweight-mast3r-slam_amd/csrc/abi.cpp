@@ -277,9 +277,12 @@ extern "C" int m3s_match(const float* X11, const float* X21, const float* D11, c
   // (matching.py:78-88); D11h is never read then.
   {
     Span sp("refine_lin", s);
-    // M3S_REFINE_INPLACE=1 (experiment): no deferred-pixel list, each wave scores its window outliers in place
+    // every wave scores its window outliers in place (no deferred list, no refine_outlier_kernel launch: on coherent
+    // inputs the list is empty and the launch alone cost ~2 us per frame; a scattered warm start, every lane an
+    // outlier, costs its waves 64 pixels x 5 levels serially). M3S_REFINE_INPLACE=0: waves with more than
+    // RT_INPLACE_MAX outliers defer them to the list and the outlier launch
     const char* inplace_env = getenv("M3S_REFINE_INPLACE");
-    const bool inplace = inplace_env != nullptr && inplace_env[0] == '1';
+    const bool inplace = !(inplace_env != nullptr && inplace_env[0] == '0');
     HIP_TRY(m3s_launch_refine_lin(D11h, D21, p1, idx_out, B, H, W, F, radius, radius > 0 ? dilation_max : 0,
                                   inplace ? nullptr : w.olist,
                                   w.ocount, screen ? w.cmax : nullptr, s),
