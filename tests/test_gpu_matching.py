@@ -141,12 +141,16 @@ def test_fused_match_ragged_and_dilations_vs_oracle(shape, dmax):
     assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
 
 
-def test_fused_match_scattered_warm_start_vs_oracle():
+@pytest.mark.parametrize("inplace", ["1", "0"])
+def test_fused_match_scattered_warm_start_vs_oracle(monkeypatch, inplace):
     """A random warm start scatters the LM results, so many refine centres fall outside their tile's
-    LDS window: exercises the deferred-outlier list + wave-per-pixel kernel (refine.hip) against the
-    oracle's sequential scan, and the in-place cooperative path through the reference op."""
+    LDS window: exercises the in-place outlier scoring (default) and, with M3S_REFINE_INPLACE=0, the deferred-outlier
+    list + wave-per-pixel kernel (refine.hip) against the oracle's sequential scan, and the in-place cooperative path
+    through the reference op."""
     from m3s.matching import match
     from m3s.synthetic import make_pair
+
+    monkeypatch.setenv("M3S_REFINE_INPLACE", inplace)
 
     H, W = 96, 128
     P = make_pair(H, W, seed=21)
