@@ -49,9 +49,6 @@ namespace m3s {
 // while chunk c is screened (the d = 2 cover is 23 x 45-47 on 97.6 % of the synthetic 512x512 tiles)
 #define RT_DROWS 26
 #define RT_DBUF (RT_DROWS * RT_PCOLS)
-#ifndef RT_HALF  // bound-screened levels on the double-buffered half-chunk window (d = 1 keeps its packed window)
-#define RT_HALF 1
-#endif
 #ifndef RT_INPLACE_MAX  // window outliers a wave scores in place at one level (more: deferred to the list)
 #define RT_INPLACE_MAX 8
 #endif
@@ -249,35 +246,6 @@ __device__ __forceinline__ void lds_dma_row(const h1* g, unsigned lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(g) : "memory");
 }
 
-// the same for one dword per lane (the half-chunk window: two lanes per pixel, 8 B of its 16-B chunk each)
-__device__ __forceinline__ void lds_dma_row4(const h1* g, unsigned lds_addr) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m0), "v"(g) : "memory");
-}
-
-// 49 candidates x one half-chunk (4 channels, 8 B per pixel) of the half-chunk window (row stride RT_COLS pixels)
-template <int D>
-__device__ __forceinline__ void screen_half(const uint2* base, const h2* q2, float* a) {
-  constexpr int G = 7;
-#pragma unroll
-  for (int i = 0; i < G; i++) {
-    uint2 c[G];
-#pragma unroll
-    for (int j = 0; j < G; j++) c[j] = base[j * D * RT_COLS + i * D];
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-      const h2* cv = reinterpret_cast<const h2*>(&c[j]);
-      float t = a[i * G + j];
-      t = __builtin_amdgcn_fdot2(q2[0], cv[0], t, false);
-      t = __builtin_amdgcn_fdot2(q2[1], cv[1], t, false);
-      a[i * G + j] = t;
-    }
-    float* ac = &a[i * G];
-    asm volatile("" : "+v"(ac[0]), "+v"(ac[1]), "+v"(ac[2]), "+v"(ac[3]), "+v"(ac[4]), "+v"(ac[5]), "+v"(ac[6]));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 // the packed window's variant: the survivors' three chunks are read from the resident LDS planes (base = candidate
 // (0,0) of this lane in plane 0), no L2 round trip; same ascending order, same strict '>'
 template <int D>
@@ -352,7 +320,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   const int x_lo = mnu - RD, x_hi = mxu + RD, y_lo = mnv - RD, y_hi = mxv + RD;
   bool packed = false, dbuf = false;  // block-uniform: every input is
   if constexpr (SCREEN && D == 1) packed = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_PROWS;
-  if constexpr (SCREEN && D == 2 && !RT_HALF) dbuf = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_DROWS;
+  if constexpr (SCREEN && D == 2) dbuf = x_hi - x_lo + 1 <= RT_PCOLS && y_hi - y_lo + 1 <= RT_DROWS;
   const int wc = (packed || dbuf) ? RT_PCOLS : RT_COLS, wr = packed ? RT_PROWS : (dbuf ? RT_DROWS : RT_ROWS);
   const int wx0 = (x_hi - x_lo + 1 <= wc) ? x_lo : t.tcu - wc / 2;
   const int wy0 = (y_hi - y_lo + 1 <= wr) ? y_lo : t.tcv - wr / 2;
@@ -475,44 +443,6 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
 #ifndef RT_NOCOMP
       if (lane_in) screen_chunk<D, RT_PCOLS>(&lds[b0], &q[8], a);
 #endif
-    } else if constexpr (RT_HALF) {
-      // six half-chunks (4 channels, 8 B per pixel), two 20 KiB buffers: half-chunk h + 1 streams in (dword DMA,
-      // two lanes per pixel) while half-chunk h is screened; the fill latency of all but the first is hidden
-      const int hx = lane >> 1, hw = lane & 1;  // lane -> (pixel of a 32-pixel half row, dword of its 8 B)
-      auto fill = [&](int hc, int buf) {
-#ifndef RT_NOLOAD
-        const int chunk = hc >> 1, half = hc & 1;
-        for (int y = wid; y < nrows; y += 4) {
-          const int gy = min(max(wy0 + y, 0), H - 1);
-          const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride + half * 4 + hw * 2;
-#pragma unroll
-          for (int k = 0; k < 2; k++) {
-            const int px = k * 32 + hx;
-            const int gxk = min(max(wx0 + px, 0), W - 1);
-            if (px < ncols)
-              lds_dma_row4(rowp + (size_t)gxk * (PLANAR ? 8 : F),
-                           t.lds_addr + (unsigned)buf * 20480u + (unsigned)(y * RT_COLS + k * 32) * 8u);
-          }
-        }
-#endif
-      };
-      const uint2* l2 = reinterpret_cast<const uint2*>(lds);
-      const int b0 = by * RT_COLS + bx;
-      fill(0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // the compiler's wait model: none of its loads in flight (dbuf path note)
-      __syncthreads();
-#pragma unroll
-      for (int hc = 0; hc < 6; hc++) {
-        if (hc < 5) fill(hc + 1, (hc + 1) & 1);
-#ifndef RT_NOCOMP
-        if (lane_in) screen_half<D>(&l2[(hc & 1) * 2560 + b0], &q[hc * 2], a);
-#endif
-        if (hc < 5) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();  // half-chunk hc + 1 landed; every wave is done with buffer hc & 1
-        }
-      }
     } else {
 #pragma unroll
       for (int chunk = 0; chunk < F / 8; chunk++) {
