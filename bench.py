@@ -441,7 +441,8 @@ def bench_ba(args, rank, world, dev, leg):
            "ms_first_lin_with_pack": spans["ba_lin_pack"] if fused else None,
            "ms_lin_per_iter": spans["ba_linearize"], "ms_solve_per_iter": spans["ba_solve"],
            "factor": {"blocks": info["factor_blocks"], "levels": info["levels"], "wide_steps": info["wide_steps"],
-                      "dense": bool(info["dense"]), "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2},
+                      "dense": bool(info["dense"]), "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2,
+                      "front_steps": info["subtree_steps"], "front_workgroups": info["subtree_workgroups"]},
            "scaling": "strong", "roofline": roof,
            "pack": {"GBps": (pack_bytes + (alg if fused else 0)) / pack_s / 1e9,
                     "frac": (pack_bytes + (alg if fused else 0)) / pack_s / 1e9 / HBM_PEAK_GBS,

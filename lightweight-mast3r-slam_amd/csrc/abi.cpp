@@ -557,10 +557,11 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_SYM_SECTIONS = 17;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_SYM_SECTIONS = 19;  // the symbolic half's sections (build_symbolic)
 constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
 constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
 constexpr int BA_SP_PLAN_BYTES = 144 * 1024;  // ba.hip SP_PLAN_BYTES: LDS of the one-workgroup factor kernel
+constexpr int BA_FRONT_LDS_BYTES = 159 * 1024;  // ba.hip FRONT_LDS_BYTES: LDS image of a frontal-phase workgroup
 constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
@@ -578,6 +579,10 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + wide-step task records
                       8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + subtree task records
                       4 * (size_t)BA_SUB_MAX_WG * BA_MAX_WIDE_STEPS +                      //   and their step table
+                      // + the frontal phase: per workgroup (<= nb) directory, header, steps; records (factor + group +
+                      // U tasks), sources and their maps (each update pair once), slot and column maps; apply table
+                      (size_t)nb * (4 + 16 + 2 * (BA_MAX_WIDE_STEPS + 1) + 4) + 8 * (nb + 2 * nLm) + 4 * nLm +
+                      ba_max_pairs(Kp) + nLm + nb + 8 * (size_t)nb + nLm +
                       2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm);  // + the dataflow schedule
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
@@ -721,6 +726,7 @@ struct PlanSym {
   size_t off[BA_SYM_SECTIONS] = {0};
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
   int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
+  int front_cut = 0, front_wgs = 0, front_napply = 0;  // frontal subtree phase (ba_front_kernel), see build_symbolic
   bool pack_deferred = false;    // the plan's pack runs inside its first linearisation (set at plan time, under g_sym_mu)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
@@ -739,24 +745,6 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   if (S.too_dense || S.sidx.size() > ba_max_pairs(Kp)) {
     Y->err = "ba: factor pattern too dense for the plan tables";
     return M3S_EINVAL;
-  }
-  // the wide steps' task records (ba_sparse_step_kernel): per task {j, b0, b1, pull group or -1} and its group's
-  // source range, so a launched task starts with its column's own loads
-  std::vector<int> step_rec;
-  {
-    const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
-    auto put = [&](int j, int g) {
-      const int* gq = g >= 0 ? &S.grp[4 * (size_t)g] : nullptr;
-      const int r[8] = {j, S.col_ptr[j], S.col_ptr[j + 1], g, gq ? gq[1] : 0, gq ? gq[2] : 0, 0, 0};
-      step_rec.insert(step_rec.end(), r, r + 8);
-    };
-    for (int l = 0; l < lmax; l++) {
-      Y->step_base[l] = (int)step_rec.size() / 8;
-      Y->step_na[l] = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
-      for (int c = l < S.nlev ? S.lev_ptr[l] : 0; c < (l < S.nlev ? S.lev_ptr[l + 1] : 0); c++)
-        put(S.lev_col[c], S.pull_grp[S.lev_col[c]]);
-      for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
-    }
   }
   // sparse or dense factorisation: measured on MI355X (scripts/ba_exp.py), the one-workgroup sparse
   // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
@@ -851,6 +839,59 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   } else {
     Y->wide_steps = legacy_split();
   }
+  // Frontal subtree phase (an option, not the default: M3S_BA_FRONT=c forces cut c, -1 the highest that fits): the
+  // steps below the cut run as ONE launch with every subtree's blocks in its workgroup's LDS (ba_front_plan), in front
+  // of the launched steps [cut, wide). The cut: at most the launched steps - 1, with workgroups that fit the LDS
+  // image and U columns that fit the factor region's unused tail (the workspace reserves the densest pattern's
+  // blocks). Measured on MI355X (DESIGN.md §4 BA): no faster than the launched steps (a step inside the workgroup
+  // costs ~5.1 us against ~5.6 us per launched step; the column tasks are issue-latency bound either way).
+  std::vector<int> fronttab, frontapply;
+  const char* fenv2 = getenv("M3S_BA_FRONT");
+  const int front_forced = fenv2 && *fenv2 ? atoi(fenv2) : 0;
+  if (front_forced != 0 && !Y->dense && Y->sub_cut == 0 && Y->wide_steps >= 2 && S.nlev >= 2) {
+    const int hi = std::min(Y->wide_steps - 1, S.nlev - 1);
+    const size_t u_cap = (ba_max_blocks(Kp) - (size_t)S.nL) * 64;
+    for (int cut = front_forced > 0 ? std::min(front_forced, hi) : hi; cut >= 1; cut--) {
+      size_t ud = 0;
+      int nap = 0;
+      const int nwg = ba_front_plan(S, cut, BA_FRONT_LDS_BYTES, &fronttab, &frontapply, &ud, &nap);
+      if (nwg > 0 && ud <= u_cap) {
+        Y->front_cut = cut;
+        Y->front_wgs = nwg;
+        Y->front_napply = nap;
+        break;
+      }
+      fronttab.clear();
+      frontapply.clear();
+      if (front_forced > 0) break;
+    }
+  }
+  std::vector<int> lev_of(S.nb, 0);
+  for (int l = 0; l < S.nlev; l++)
+    for (int c = S.lev_ptr[l]; c < S.lev_ptr[l + 1]; c++) lev_of[S.lev_col[c]] = l;
+  if (Y->front_cut > 0)  // the U columns replace the pull groups of the columns at the cut (their sources lie below)
+    for (int j = 0; j < S.nb; j++)
+      if (lev_of[j] == Y->front_cut) S.pull_grp[j] = -1;
+  // the wide steps' task records (ba_sparse_step_kernel): per task {j, b0, b1, pull group or -1} and its group's
+  // source range, so a launched task starts with its column's own loads. With the frontal phase the steps <= cut
+  // carry no update groups (their sources lie below the cut: the U columns replaced them).
+  std::vector<int> step_rec;
+  {
+    auto put = [&](int j, int g) {
+      const int* gq = g >= 0 ? &S.grp[4 * (size_t)g] : nullptr;
+      const int r[8] = {j, S.col_ptr[j], S.col_ptr[j + 1], g, gq ? gq[1] : 0, gq ? gq[2] : 0, 0, 0};
+      step_rec.insert(step_rec.end(), r, r + 8);
+    };
+    for (int l = 0; l < lmax; l++) {
+      Y->step_base[l] = (int)step_rec.size() / 8;
+      Y->step_na[l] = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
+      for (int c = l < S.nlev ? S.lev_ptr[l] : 0; c < (l < S.nlev ? S.lev_ptr[l + 1] : 0); c++)
+        put(S.lev_col[c], S.pull_grp[S.lev_col[c]]);
+      if (l > Y->front_cut)
+        for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
+      Y->step_tasks[l] = (int)step_rec.size() / 8 - Y->step_base[l];
+    }
+  }
   // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
   if (flow_on) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
   Y->flow = sched.empty() ? 0 : 1;
@@ -865,7 +906,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
                                                    &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
                                                    &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
-                                                   &step_rec, &subtab};
+                                                   &step_rec, &subtab,  &fronttab,  &frontapply};
   size_t total = 0;
   for (int k = 0; k < BA_SYM_SECTIONS; k++) {
     Y->off[k] = total;
@@ -947,7 +988,7 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
       (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
       (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
       (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec,
-      (const void**)&a.sub_tab};
+      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply};
   for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
@@ -957,6 +998,10 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   a.flow = Y->flow;
   a.sub_cut = Y->sub_cut;
   a.sub_wgs = Y->sub_wgs;
+  a.front_cut = Y->front_cut;
+  a.front_wgs = Y->front_wgs;
+  a.front_napply = Y->front_napply;
+  a.front_u = a.L + (size_t)Y->nL * 64;
   return a;
 }
 
@@ -1381,8 +1426,8 @@ extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   info[5] = P->n_targets;
   info[6] = P->e1 - P->e0;
   info[7] = P->Kp;
-  info[8] = Y->sub_cut;
-  info[9] = Y->sub_wgs;
+  info[8] = Y->front_wgs > 0 ? Y->front_cut : Y->sub_cut;
+  info[9] = Y->front_wgs > 0 ? Y->front_wgs : Y->sub_wgs;
   return M3S_OK;
 }
 

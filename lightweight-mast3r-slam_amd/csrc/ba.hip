@@ -1143,6 +1143,207 @@ __global__ void __launch_bounds__(SUB_WAVES * 64) ba_subtree_kernel(BaArgs a) {
   }
 }
 
+// Frontal subtree phase (ba_pattern.h ba_front_plan): one workgroup per elimination subtree below the cut, its factor
+// blocks (rows 0..6 of each 8x8 block, FB doubles), rhs rows and translated task tables resident in LDS. Steps
+// [0, cut) run level by level (a barrier between steps, every hand-off an LDS access); then each target column above
+// the cut gets this subtree's summed update U (sources ascending) in a scratch column shaped like the target's rows;
+// the factor and rhs rows go back to L / y once.
+constexpr int FRONT_WAVES = 8;
+constexpr int FRONT_LDS_BYTES = 159 * 1024;
+constexpr int FB = 56;
+
+struct FrontCtx {
+  double* L;        // nslots blocks of FB doubles
+  double* Y;        // ncols rhs rows of 8 doubles
+  const int* src;   // int4 {slot of L_jk, yslot of k, sidx offset, 0}
+  const int* sidx;  // per source, per block of the target: slot or -1
+};
+
+// row p of a task's target: block p / 7 of the target (slot0 ...), the rhs row after them
+__device__ __forceinline__ double* fr_row(const FrontCtx& F, int slot0, int nblk, int ys, int p) {
+  return p < 7 * nblk ? F.L + (slot0 + p / 7) * FB + (p - 7 * (p / 7)) * 8 : F.Y + ys * 8;
+}
+
+// v -= x L_jk^T for the task's sources [s0, s1) (row p of a target with nblk blocks; lanes without the row idle).
+// L_jk is read straight from LDS (rows of stride 8; every lane reads the same words: broadcast).
+__device__ __forceinline__ void fr_sources(const FrontCtx& F, int s0, int s1, int nblk, int p, bool act,
+                                           double (&v)[8]) {
+  for (int e = s0; e < s1; e++) {
+    const int4 s = reinterpret_cast<const int4*>(F.src)[e];
+    const double* xr = nullptr;
+    if (act) {
+      if (p == 7 * nblk) {
+        xr = F.Y + s.y * 8;
+      } else {
+        const int sb = F.sidx[s.z + p / 7];
+        xr = sb >= 0 ? F.L + sb * FB + (p - 7 * (p / 7)) * 8 : nullptr;
+      }
+    }
+    if (xr) {
+      double x[8];
+      ld_row(x, xr);
+      const double* bjk = F.L + s.x * FB;
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        const double* bc = bjk + c * 8;
+        const double p0 = fma(x[0], bc[0], x[1] * bc[1]);
+        const double p1 = fma(x[2], bc[2], x[3] * bc[3]);
+        const double p2 = fma(x[4], bc[4], x[5] * bc[5]);
+        v[c] -= (p0 + p1) + fma(x[6], bc[6], p2);
+      }
+    }
+  }
+}
+
+// one task of a front workgroup: r = {kind, slot0, nblk, yslot, src begin, src end, U offset}. kind 0: pull the
+// sources, then the column's register-row factorisation (as sp_factor_column_at: lanes 0..6 the diagonal rows, the
+// triangular solve for the rows below, the forward substitution for the rhs row; passes of 64 rows); kind 1: an update
+// group into an LDS column; kind 2: the U column of a target above the cut (v = 0, the sources, stored to U)
+__device__ __forceinline__ void fr_task(const FrontCtx& F, const int* r, double* U, int lane, int* bad) {
+  const int kind = r[0], slot0 = r[1], nblk = r[2], ys = r[3], s0 = r[4], s1 = r[5];
+  const int nrow = 7 * nblk + 1;
+  double inv[7], lo[21];
+  bool fail = false;
+  for (int base = 0; base < nrow; base += 64) {
+    const int p = base + lane;
+    const bool act = p < nrow;
+    double v[8];
+    double* rp = nullptr;
+    if (kind == 2) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) v[c] = 0.0;
+    } else {
+      rp = act ? fr_row(F, slot0, nblk, ys, p) : nullptr;
+      if (act) {
+        ld_row(v, rp);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = 0.0;
+      }
+    }
+    fr_sources(F, s0, s1, nblk, p, act, v);
+    if (kind == 0) {
+      if (base == 0) {
+#pragma unroll
+        for (int m = 0; m < 7; m++) {
+          double d = bcast_lane(v[m], m);
+          if (!(d > 0.0)) {
+            fail = true;
+            d = 1.0;
+          }
+          inv[m] = rsqrt_nr(d);
+          const double l = v[m] * inv[m];
+          v[m] = lane == m ? d * inv[m] : l;
+#pragma unroll
+          for (int c = m + 1; c < 7; c++) {
+            const double lc = bcast_lane(l, c);
+            lo[c * (c - 1) / 2 + m] = lc;
+            v[c] = fma(-l, lc, v[c]);
+          }
+        }
+        if (lane < 7) {
+          double iv = inv[0];
+#pragma unroll
+          for (int m = 1; m < 7; m++) iv = lane == m ? inv[m] : iv;
+          v[7] = iv;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 7; m++) {
+          v[m] *= inv[m];
+#pragma unroll
+          for (int c = m + 1; c < 7; c++) v[c] = fma(-v[m], lo[c * (c - 1) / 2 + m], v[c]);
+        }
+      }
+    }
+    if (act) {
+      if (kind == 2)
+        st_row(U + r[6] + (size_t)p * 8, v);
+      else
+        st_row(rp, v);
+    }
+  }
+  if (fail && lane == 0) atomicOr(bad, BA_BAD_LLT);
+}
+
+__global__ void __launch_bounds__(FRONT_WAVES * 64) ba_front_kernel(BaArgs a) {
+  __shared__ __attribute__((aligned(16))) double s_front[FRONT_LDS_BYTES / 8];
+  if (*a.done) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  constexpr int NT = FRONT_WAVES * 64;
+  const int4 dir = reinterpret_cast<const int4*>(a.front_tab)[blockIdx.x];
+  const int* gt = a.front_tab + dir.x;
+  const int nslots = gt[0], ncols = gt[1], cut = gt[2];
+  double* L = s_front;
+  double* Y = s_front + nslots * FB;
+  int* T = reinterpret_cast<int*>(Y + ncols * 8);
+  {  // the table (16-B sections, dir.y a multiple of 4)
+    const int4* g4 = reinterpret_cast<const int4*>(gt);
+    int4* t4 = reinterpret_cast<int4*>(T);
+    for (int i = tid; i < dir.y / 4; i += NT) t4[i] = g4[i];
+  }
+  __syncthreads();
+  const int* slot_gb = T + T[7];
+  const int* colj = T + T[8];
+  double2* L2 = reinterpret_cast<double2*>(L);
+  double2* Y2 = reinterpret_cast<double2*>(Y);
+  const double2* gL = reinterpret_cast<const double2*>(a.L);
+  const double2* gy = reinterpret_cast<const double2*>(a.y);
+  for (int i = tid; i < nslots * (FB / 2); i += NT) {
+    const int s = i / (FB / 2), e = i - (FB / 2) * s;
+    L2[i] = gL[(size_t)slot_gb[s] * 32 + e];
+  }
+  for (int i = tid; i < ncols * 4; i += NT) Y2[i] = gy[(size_t)colj[i >> 2] * 4 + (i & 3)];
+  __syncthreads();
+  const FrontCtx F{L, Y, T + T[5], T + T[6]};
+  const int* rec = T + T[4];
+  const int2* steps = reinterpret_cast<const int2*>(T + 16);
+  for (int l = 0; l <= cut; l++) {  // l == cut: the U columns (LDS read-only from here)
+    const int2 st = steps[l];
+    for (int t = w; t < st.y; t += FRONT_WAVES) fr_task(F, rec + 8 * (st.x + t), a.front_u, lane, a.bad);
+    if (l < cut && st.y > 0) __syncthreads();
+  }
+  double2* gLw = reinterpret_cast<double2*>(a.L);
+  double2* gyw = reinterpret_cast<double2*>(a.y);
+  for (int i = tid; i < nslots * (FB / 2); i += NT) {
+    const int s = i / (FB / 2), e = i - (FB / 2) * s;
+    gLw[(size_t)slot_gb[s] * 32 + e] = L2[i];
+  }
+  for (int i = tid; i < ncols * 4; i += NT) gyw[(size_t)colj[i >> 2] * 4 + (i & 3)] = Y2[i];
+}
+
+// the U columns into L / y: one workgroup per target above the cut, the workgroups' columns in ascending order
+__global__ void __launch_bounds__(64) ba_front_apply_kernel(BaArgs a) {
+  if (*a.done) return;
+  const int lane = threadIdx.x;
+  const int* e = a.front_apply + 8 * blockIdx.x;
+  const int j = e[0], b0 = e[1], nblk = e[2], u0 = e[3], u1 = e[4];
+  const int* ul = a.front_apply + 8 * a.front_napply;
+  const int nrow = 7 * nblk + 1;
+  for (int p = lane; p < nrow; p += 64) {
+    double* rp = p < 7 * nblk ? a.L + (size_t)(b0 + p / 7) * 64 + (p - 7 * (p / 7)) * 8 : a.y + (size_t)j * 8;
+    double v[8];
+    ld_row(v, rp);
+    int u = u0;
+    for (; u + 4 <= u1; u += 4) {  // four U rows in flight, added in list order
+      double x[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; q++) ld_row(x[q], a.front_u + ul[u + q] + (size_t)p * 8);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] += x[q][c];
+    }
+    for (; u < u1; u++) {
+      double x[8];
+      ld_row(x, a.front_u + ul[u] + (size_t)p * 8);
+#pragma unroll
+      for (int c = 0; c < 8; c++) v[c] += x[c];
+    }
+    st_row(rp, v);
+  }
+}
+
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
 __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
@@ -1344,6 +1545,7 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
                                           const int* step_base, const int* step_na, hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
   static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
+  static_assert(m3s::FRONT_LDS_BYTES == 159 * 1024, "abi.cpp BA_FRONT_LDS_BYTES");
   // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column
   const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64;
   const bool flow_fits = a->flow && lds + (size_t)a->nb * 12 <= (size_t)m3s::SP_PLAN_BYTES;
@@ -1351,7 +1553,13 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
   // one when that schedule fits: a level-synchronous run would re-factor the subtrees' columns)
   if (a->sub_wgs > 0 && !flow_fits) return hipErrorInvalidValue;
   if (a->sub_wgs > 0) hipLaunchKernelGGL(m3s::ba_subtree_kernel, dim3(a->sub_wgs), dim3(m3s::SUB_WAVES * 64), 0, s, *a);
-  for (int l = 0; l < a->wide_steps; l++)
+  // the frontal subtree phase: steps [0, front_cut) in LDS, then the U columns into the targets above the cut; the
+  // launched steps resume at front_cut (their records leave out the groups the U columns replaced)
+  if (a->front_wgs > 0) {
+    hipLaunchKernelGGL(m3s::ba_front_kernel, dim3(a->front_wgs), dim3(m3s::FRONT_WAVES * 64), 0, s, *a);
+    if (a->front_napply > 0) hipLaunchKernelGGL(m3s::ba_front_apply_kernel, dim3(a->front_napply), dim3(64), 0, s, *a);
+  }
+  for (int l = a->front_wgs > 0 ? a->front_cut : 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],
                          step_na[l]);

@@ -463,3 +463,161 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
   }
   return makespan;
 }
+
+int ba_front_plan(const BaPattern& P, int cut, size_t lds_bytes, std::vector<int>* tab, std::vector<int>* apply,
+                  size_t* u_doubles, int* napply) {
+  const int nb = P.nb;
+  tab->clear();
+  apply->clear();
+  *u_doubles = 0;
+  *napply = 0;
+  cut = std::min(cut, P.nlev);
+  if (nb <= 0 || cut <= 0) return 0;
+  const std::vector<int> lev = col_levels(P);
+  std::vector<int> root(nb, -1);
+  for (int j = nb - 1; j >= 0; j--) {
+    if (lev[j] >= cut) continue;
+    const int p = P.col_ptr[j + 1] - P.col_ptr[j] > 1 ? P.rowL[P.col_ptr[j] + 1] : -1;
+    root[j] = (p < 0 || lev[p] >= cut) ? j : root[p];
+  }
+  std::vector<int> roots, sid(nb, -1);
+  for (int j = 0; j < nb; j++)
+    if (root[j] == j) {
+      sid[j] = (int)roots.size();
+      roots.push_back(j);
+    }
+  const int ns = (int)roots.size();
+  std::vector<std::vector<int>> cols(ns);
+  for (int j = 0; j < nb; j++)
+    if (root[j] >= 0) cols[sid[root[j]]].push_back(j);
+  auto nblk = [&](int j) { return P.col_ptr[j + 1] - P.col_ptr[j]; };
+  std::vector<int> gslot(P.nL, -1), ycol(nb, -1);
+  std::vector<int> slot(nb, -1), stamp(nb, 0);  // block of the current source column at a row (build_pattern's trick)
+  std::vector<std::vector<int>> ulist(nb);      // per target above the cut: U offsets, workgroups ascending
+  std::vector<std::vector<int>> by_tgt(nb);
+  size_t uoff = 0;
+  std::vector<int> dir((size_t)4 * ns, 0), body;
+  for (int s = 0; s < ns; s++) {
+    const std::vector<int>& C = cols[s];
+    std::vector<int> slot_gb, colj, rec, src, sx;
+    for (int j : C) {
+      ycol[j] = (int)colj.size();
+      colj.push_back(j);
+      for (int b = P.col_ptr[j]; b < P.col_ptr[j + 1]; b++) {
+        gslot[b] = (int)slot_gb.size();
+        slot_gb.push_back(b);
+      }
+    }
+    // one translated source: L_jk's slot, k's rhs row, and per block of the target j the slot of column k's block
+    // at that row (-1 where struct(k) misses it)
+    auto put_src = [&](int j, int k) {
+      int bjk = -1;
+      for (int q = P.col_ptr[k] + 1; q < P.col_ptr[k + 1]; q++) {
+        slot[P.rowL[q]] = q;
+        stamp[P.rowL[q]] = k + 1;
+        if (P.rowL[q] == j) bjk = q;
+      }
+      src.push_back(gslot[bjk]);
+      src.push_back(ycol[k]);
+      src.push_back((int)sx.size());
+      src.push_back(0);
+      for (int b = P.col_ptr[j]; b < P.col_ptr[j + 1]; b++) {
+        const int i = P.rowL[b];
+        sx.push_back(stamp[i] == k + 1 ? gslot[slot[i]] : -1);
+      }
+    };
+    auto put_rec = [&](int kind, int j, int s0, int s1, long long u) {
+      const int r[8] = {kind, kind == 2 ? 0 : gslot[P.col_ptr[j]], nblk(j), kind == 2 ? 0 : ycol[j], s0, s1,
+                        (int)u, 0};
+      rec.insert(rec.end(), r, r + 8);
+    };
+    auto grp_sources = [&](int j, int g) {  // an existing group's sources (all inside this subtree), translated
+      const int s0 = (int)src.size() / 4;
+      for (int e = P.grp[4 * (size_t)g + 1]; e < P.grp[4 * (size_t)g + 2]; e++) put_src(j, P.src[4 * (size_t)e + 1]);
+      return s0;
+    };
+    std::vector<int> steps;
+    for (int l = 0; l < cut; l++) {
+      const int first = (int)rec.size() / 8;
+      for (int j : C)
+        if (lev[j] == l) {
+          const int g = P.pull_grp[j];
+          const int s0 = g >= 0 ? grp_sources(j, g) : (int)src.size() / 4;
+          put_rec(0, j, s0, (int)src.size() / 4, 0);
+        }
+      for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
+        const int j = P.grp[4 * (size_t)t];
+        if (lev[j] >= cut || sid[root[j]] != s) continue;
+        const int s0 = grp_sources(j, t);
+        put_rec(1, j, s0, (int)src.size() / 4, 0);
+      }
+      steps.push_back(first);
+      steps.push_back((int)rec.size() / 8 - first);
+    }
+    // U tasks: every target above the cut, its sources (this subtree's columns) ascending
+    std::vector<int> tg;
+    for (int k : C)
+      for (int b = P.col_ptr[k] + 1; b < P.col_ptr[k + 1]; b++) {
+        const int j = P.rowL[b];
+        if (lev[j] < cut) continue;
+        if (by_tgt[j].empty()) tg.push_back(j);
+        by_tgt[j].push_back(k);
+      }
+    std::sort(tg.begin(), tg.end());
+    const int ufirst = (int)rec.size() / 8;
+    for (int j : tg) {
+      const int s0 = (int)src.size() / 4;
+      for (int k : by_tgt[j]) put_src(j, k);
+      by_tgt[j].clear();
+      if (uoff > (size_t)INT32_MAX - 64 * (size_t)P.nL) return 0;
+      put_rec(2, j, s0, (int)src.size() / 4, (long long)uoff);
+      ulist[j].push_back((int)uoff);
+      uoff += (size_t)8 * (7 * nblk(j) + 1);
+    }
+    steps.push_back(ufirst);
+    steps.push_back((int)rec.size() / 8 - ufirst);
+    for (int j : C) ycol[j] = -1;
+    for (int b : slot_gb) gslot[b] = -1;
+    // the table, 16-B aligned sections
+    std::vector<int> t(16, 0);
+    auto sec = [&](const std::vector<int>& v) {
+      const int o = (int)t.size();
+      t.insert(t.end(), v.begin(), v.end());
+      while (t.size() % 4) t.push_back(0);
+      return o;
+    };
+    sec(steps);
+    t[4] = sec(rec);
+    t[5] = sec(src);
+    t[6] = sec(sx);
+    t[7] = sec(slot_gb);
+    t[8] = sec(colj);
+    t[0] = (int)slot_gb.size();
+    t[1] = (int)colj.size();
+    t[2] = cut;
+    const size_t lds = (size_t)slot_gb.size() * 56 * 8 + colj.size() * 64 + t.size() * 4;
+    if (lds > lds_bytes) {
+      tab->clear();
+      return 0;
+    }
+    dir[4 * (size_t)s] = (int)body.size();
+    dir[4 * (size_t)s + 1] = (int)t.size();
+    body.insert(body.end(), t.begin(), t.end());
+  }
+  for (int s = 0; s < ns; s++) dir[4 * (size_t)s] += 4 * ns;
+  tab->assign(dir.begin(), dir.end());
+  tab->insert(tab->end(), body.begin(), body.end());
+  // apply entries (targets ascending) and their U lists
+  std::vector<int> ent, lists;
+  for (int j = 0; j < nb; j++) {
+    if (ulist[j].empty()) continue;
+    const int r[8] = {j, P.col_ptr[j], nblk(j), (int)lists.size(), (int)(lists.size() + ulist[j].size()), 0, 0, 0};
+    ent.insert(ent.end(), r, r + 8);
+    lists.insert(lists.end(), ulist[j].begin(), ulist[j].end());
+  }
+  *napply = (int)ent.size() / 8;
+  apply->assign(ent.begin(), ent.end());
+  apply->insert(apply->end(), lists.begin(), lists.end());
+  *u_doubles = uoff;
+  return ns;
+}

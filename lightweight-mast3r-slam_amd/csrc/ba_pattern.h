@@ -75,3 +75,25 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
 // tasks (first), 0}, then 8-int task records {j, b0, b1, pull group or -1 (factor task) | group, src begin, src end,
 // 0, 0}. Returns the number of workgroups; *cost_us = the estimated finish time of the slowest workgroup.
 int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vector<int>* tab, double* cost_us);
+
+// Frontal subtree phase (ba_front_kernel / ba_front_apply_kernel, ba.hip): the columns below elimination-tree level
+// `cut` fall into independent subtrees; ONE launch runs one workgroup per subtree with the subtree's factor blocks,
+// rhs rows and translated task tables resident in LDS (global -> LDS once, every step an LDS hand-off behind a
+// workgroup barrier, LDS -> global once). The subtree's contributions to the columns above the cut are not applied as
+// the level's update groups: each workgroup sums them per target column (its sources ascending) into a dense update
+// column U_(W,j) laid out like column j's rows (rhs last) in a scratch region, and a second launch adds the U columns
+// of every target (workgroups ascending) into L / y. The steps [cut, ...) then run without the groups whose sources
+// lie below the cut (every step <= cut; the factor tasks of level `cut` pull nothing). Deterministic (fixed orders),
+// but not bit-identical to the group schedules (the below-cut sums are associated per subtree).
+// Layout of `tab` (ints): per workgroup an int4 {table offset, table ints (multiple of 4), 0, 0}, then the tables:
+//   [16-int header: nslots, ncols, cut, 0, off_rec, off_src, off_sidx, off_slotgb, off_colj, 0...]
+//   [cut + 1 int2 steps {first record, tasks}; entry `cut` = the U tasks]
+//   [records 8 ints: {kind 0 factor | 1 group | 2 U, slot0, nblk, yslot, src begin, src end, U offset, 0}]
+//   [sources int4 {slot of L_jk, yslot of k, sidx offset, 0}] [sidx: per source, per block of the target: slot or -1]
+//   [slot -> global block] [yslot -> column]
+// LDS image per workgroup: nslots blocks of 56 doubles (rows 0..6 of the 8x8 block), ncols rhs rows of 8 doubles,
+// then the table; lds_bytes bounds it. `apply` (ints): napply 8-int entries {j, first block, nblk, list begin, list
+// end, 0, 0, 0} (targets ascending), then the lists of U offsets (doubles into the scratch region). Returns the
+// number of workgroups (0: the cut does not fit); *u_doubles = the scratch size, *napply = the apply entries.
+int ba_front_plan(const BaPattern& P, int cut, size_t lds_bytes, std::vector<int>* tab, std::vector<int>* apply,
+                  size_t* u_doubles, int* napply);

@@ -73,6 +73,12 @@ struct BaArgs {
                           // task records (2 x int4, as step_rec)
   int sub_cut;            // steps [0, sub_cut) run in the subtree launch (0: none)
   int sub_wgs;            // its workgroups
+  const int* front_tab;   // frontal subtree phase (ba_pattern.h ba_front_plan): per workgroup {table offset, ints}, tables
+  const int* front_apply; // its U columns per target above the cut: 8-int entries, then the U offset lists
+  double* front_u;        // U scratch (doubles; the factor region's tail past the plan's nL blocks)
+  int front_cut;          // steps [0, front_cut) ran in the front launch (0: none)
+  int front_wgs;          // its workgroups
+  int front_napply;       // apply entries
   const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, sched, staged into LDS by the factor kernel
   int plan_bytes;
   const int* asm_ptr;     // (nL+1) assembly CSR: edge*2 + (sign<0), edge order

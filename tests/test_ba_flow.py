@@ -54,3 +54,43 @@ def test_subtree_phase_on_trajectory_graphs(checker, tmp_path, traj, sub):
     out = subprocess.run([checker, "-f", str(f), "0", str(sub)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
     assert " sub 0 " not in out.stdout, out.stdout  # these graphs do get a subtree phase
+
+
+@pytest.fixture(scope="module")
+def front_checker(tmp_path_factory):
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path_factory.mktemp("front") / "ba_front_check")
+    subprocess.check_call([cxx, "-O2", "-std=c++17", "-I", CSRC, os.path.join(REPO, "scripts", "ba_front_check.cpp"),
+                           os.path.join(CSRC, "ba_pattern.cpp"), "-o", exe])
+    return exe
+
+
+# (K, loop edges per keyframe, seed, cut): random loop graphs, a pure chain, tiny graphs, cuts past the tree height
+FRONT_CASES = [(256, 3, 1, 1), (256, 3, 1, 2), (64, 2, 4, 3), (128, 0, 1, 20), (3, 0, 1, 1), (2, 0, 1, 1),
+               (97, 1, 7, 5), (97, 1, 7, 200), (300, 1, 9, 12)]
+
+
+@pytest.mark.parametrize("K,loops,seed,cut", FRONT_CASES)
+def test_front_phase_solves_like_dense_cholesky(front_checker, K, loops, seed, cut):
+    """The frontal subtree phase's translated tables (ba_front_plan), interpreted with ba_front_kernel's semantics,
+    then the U columns, the remaining steps without the replaced groups and the back substitution: the solution of a
+    random SPD system on the plan's pattern matches a dense Cholesky solve (and the all-groups factorisation)."""
+    out = subprocess.run([front_checker, str(K), str(loops), str(seed), str(cut)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("traj,cut", [("chess", 8), ("chess", 18), ("euroc", 8), ("euroc", 14)])
+def test_front_phase_on_trajectory_graphs(front_checker, tmp_path, traj, cut):
+    """C5 / C4 trajectory graphs at cuts that fit the workgroup's LDS image."""
+    import sys
+
+    sys.path.insert(0, os.path.join(REPO, "lightweight-mast3r-slam_amd"))
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
+
+    G = make_traj_graph((chess_poses if traj == "chess" else euroc_poses)(256), 24, 32, seed=1)
+    f = tmp_path / "edges.txt"
+    f.write_text("".join(f"{a} {b}\n" for a, b in zip(G["ii"].tolist(), G["jj"].tolist())))
+    out = subprocess.run([front_checker, "-f", str(f), str(cut)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("OK") and " nwg 0 " not in out.stdout, out.stdout + out.stderr
