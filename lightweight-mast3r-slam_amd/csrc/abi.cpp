@@ -887,7 +887,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
       Y->step_na[l] = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
       for (int c = l < S.nlev ? S.lev_ptr[l] : 0; c < (l < S.nlev ? S.lev_ptr[l + 1] : 0); c++)
         put(S.lev_col[c], S.pull_grp[S.lev_col[c]]);
-      if (l > Y->front_cut)
+      if (Y->front_cut == 0 || l > Y->front_cut)  // (step 0 has no groups: sources at level -1)
         for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
       Y->step_tasks[l] = (int)step_rec.size() / 8 - Y->step_base[l];
     }
