@@ -379,7 +379,7 @@ def bench_ba(args, rank, world, dev, leg):
     n_e = e1 - e0
     rec_bytes = BA_REC_BYTES + (4 if mode == "rays" else 0)  # rays: + |Xi| (the record holds the unit ray)
     alg = n_e * N * rec_bytes + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
-    pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}>", pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
+    pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}, false>", pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     traffic = pmc["traffic_bytes"] if pmc else None
     roof = {"kernel": "ba_lin_kernel + ba_edge_kernel", "bound": "hbm", "achieved": alg / lin_s / 1e9,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / lin_s / 1e9 / HBM_PEAK_GBS,
@@ -433,7 +433,7 @@ def bench_ba(args, rank, world, dev, leg):
     pack_s = (spans["ba_lin_pack"] if fused else spans["ba_pack"]) * 1e-3
     pack_bytes = n_e * N * (BA_PACK_EDGE_BYTES + (4 if mode == "rays" else 0)) + args.ba_kf * N * BA_PACK_KF_BYTES
     pack_pmc = pmc_entry(f"ba_pack_kernel<{1 if mode == 'rays' else 2}>",
-                         pattern=f"r[0-9][0-9]_ba{'_c4' if leg == 'C4' else ''}_pmc.json")
+                         pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     out = {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
            "points_per_kf": N, "shape": [H, W], "mode": mode, "trajectory": L["traj"], "iters": args.ba_iters,
            "ms_per_call": el * 1e3, "ms_setup": setup * 1e3, "ms_per_iter": (el - setup) / args.ba_iters * 1e3,

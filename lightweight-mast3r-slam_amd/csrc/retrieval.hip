@@ -178,7 +178,7 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
       // the compiler's own global_load_lds sequences keep one instruction there)
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0),
                    "v"(qa + (size_t)s * RQ_QU + i * 64)
-                   : "memory");  // m0 is reserved (never allocated) by the compiler: no clobber needed
+                   : "memory", "m0");  // m0 clobbered: the compiler must not keep its own M0 value live across it
     }
   };
   // codebook: global -> VGPR two k-steps ahead (a 3-slot register ring), by inline-asm loads the compiler does

@@ -181,7 +181,9 @@ def ptr(t):
 _WS = {}
 
 
-_WS_RELEASE = {"track": "m3s_track_release", "ba": "m3s_ba_plan_release"}  # key -> the ABI call that forgets a dropped buffer
+# key -> the ABI call that forgets a dropped buffer (BA workspaces are not cached here: HipShard / RecordCache own and
+# release theirs)
+_WS_RELEASE = {"track": "m3s_track_release"}
 
 
 def workspace(key, nbytes, device, stream):

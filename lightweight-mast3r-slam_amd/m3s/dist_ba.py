@@ -24,6 +24,7 @@ import torch.distributed as dist
 from m3s import _lib
 
 BA_MODES = {"points": 0, "rays": 1, "calib": 2}
+M3S_ESTALL = -4  # include/m3s.h
 
 
 def shard_range(E, rank, world):
@@ -160,6 +161,16 @@ class HipShard:
         _lib.check(self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev)))
         return it.value
 
+    def stalled(self):
+        """True when this rank's factor schedule stalled (M3S_ESTALL: its GN loop stopped); any other error
+        raises. One readback (syncs the stream)."""
+        it = ctypes.c_int()
+        rc = self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev))
+        if rc == M3S_ESTALL:
+            return True
+        _lib.check(rc)
+        return False
+
 
 def run_sharded(shard, max_iter, group=None):
     """GN loop of one rank: linearise shard -> all-reduce edge sums -> identical solve/retract.
@@ -172,6 +183,18 @@ def run_sharded(shard, max_iter, group=None):
         if reduce:
             dist.all_reduce(shard.edge_sums, op=dist.ReduceOp.SUM, group=group)
         shard.solve()
+    # The stall decision is global: a rank whose bounded factor-schedule wait timed out stops its own loop (its
+    # edge-sum rows stay zero), so its peers solved without that shard. One MAX all-reduce of the flag after the loop
+    # makes every rank raise together, instead of the stalled rank alone (whose peers would then wait for it at their
+    # next collective).
+    stalled = bool(shard.stalled()) if hasattr(shard, "stalled") else False
+    if reduce:
+        flag = torch.tensor([1.0 if stalled else 0.0], dtype=torch.float64, device=shard.edge_sums.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        stalled = bool(flag.item() > 0.0)
+    if stalled:
+        raise RuntimeError(f"m3s error {M3S_ESTALL}: ba: a factor-schedule hand-off stalled on a rank (bounded wait "
+                           "timed out); the GN loop stopped and the poses are not valid")
     return shard
 
 
@@ -193,6 +216,5 @@ def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx, valid, Q, cfg, max_iter
                      reuse=reuse, cache=cache)
     if info is not None:
         info["packed_edges"], info["changed_keyframes"] = shard.reuse_info()
-    run_sharded(shard, max_iter, group)
-    shard.iterations()  # one readback: raises RuntimeError (M3S_ESTALL) if a factor-schedule wait timed out
+    run_sharded(shard, max_iter, group)  # raises RuntimeError (M3S_ESTALL) on every rank if any rank stalled
     return [shard.dx]

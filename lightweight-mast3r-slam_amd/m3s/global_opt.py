@@ -128,11 +128,13 @@ class FactorGraph:
     @staticmethod
     def _pin(cfg):
         """cfg.pin: the C++ solvers fix exactly one pose (num_fix = 1, gn_kernels.cu:741,1157,1566) while the
-        Python slices the write-back by cfg.pin (global_opt.py:125,161), so any other pin would write poses the
-        solve held fixed (or drop solved ones): rejected (SURVEY.md §8 a-note 8)."""
-        pin = cfg["pin"]
-        if pin != 1:
-            raise ValueError(f"local_opt.pin = {pin}: only pin = 1 is supported (the solver fixes one pose)")
+        Python slices the write-back by cfg.pin (global_opt.py:125,161). pin = 1 is the configured value
+        (config/base.yaml:36). pin = 0 is accepted as the reference runs it: pose 0 stays fixed in the solve, so writing
+        T_WCs[0:] back writes it unchanged, and a graph with one keyframe has nothing to solve (the early return uses
+        max(pin, 1)). pin > 1 would drop solved poses from the write-back: rejected (SURVEY.md §8 a-note 8)."""
+        pin = int(cfg["pin"])
+        if pin not in (0, 1):
+            raise ValueError(f"local_opt.pin = {pin}: only pin = 0 or 1 is supported (the solver fixes one pose)")
         return pin
 
     def _sharded(self):
@@ -157,7 +159,7 @@ class FactorGraph:
         cfg = self.cfg
         pin = self._pin(cfg)
         unique_kf_idx = self.get_unique_kf_idx()
-        if unique_kf_idx.numel() <= pin:
+        if unique_kf_idx.numel() <= max(pin, 1):
             return
         ii, jj, idx_ii2jj, valid_match, Q_ii2jj = self.prep_two_way_edges()
         rk = self._reuse_kw(unique_kf_idx)
@@ -190,7 +192,7 @@ class FactorGraph:
         K = self.K
         pin = self._pin(cfg)
         unique_kf_idx = self.get_unique_kf_idx()
-        if unique_kf_idx.numel() <= pin:
+        if unique_kf_idx.numel() <= max(pin, 1):
             return
         Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
         img_size = frame_img_size(self.frames[0])

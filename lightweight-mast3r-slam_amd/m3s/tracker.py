@@ -142,7 +142,7 @@ class FrameTracker:
     # ------------------------------------------------------------------ fused track
     def track(self, frame):
         """tracker.py:28-127."""
-        keyframe = self.keyframes.last_keyframe()
+        keyframe, kf_slot = self._last_keyframe()
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = mast3r_match_asymmetric(
             self.model, frame, keyframe, idx_i2j_init=self.idx_f2k)
         # tracker.py:45 clones; the fused matcher returns a fresh tensor that nothing writes to, so the
@@ -166,7 +166,7 @@ class FrameTracker:
         # into the slot itself; the rest of the record (img, uimg, feat, pos, T_WC) is what the slot already holds
         slot = None
         if fuse_fused and self.slot_writeback:
-            slot = slot_rows(self.keyframes, keyframe, len(self.keyframes) - 1)
+            slot = slot_rows(self.keyframes, keyframe, kf_slot)
 
         res, T_f, T_r = self._run_track(
             idx=idx_f2k, valid=valid_match_k, Xf=frame.X_canon, Cf=frame.C, Nf=frame.N, Qff=Qff,
@@ -191,7 +191,7 @@ class FrameTracker:
         else:
             keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf)
         if slot is None:  # write back the filtered pointmap (tracker.py:101)
-            self.keyframes[len(self.keyframes) - 1] = keyframe
+            self.keyframes[kf_slot] = keyframe
 
         n = res.N
         match_frac_k = res.n_valid_kf / n
@@ -204,6 +204,22 @@ class FrameTracker:
         else:
             Ck_avg, Cf_avg = keyframe.get_average_conf(), frame.get_average_conf()
         return (new_kf, [keyframe.X_canon, Ck_avg, frame.X_canon, Cf_avg, Qkf, Qff], False)
+
+    def _last_keyframe(self):
+        """(keyframes.last_keyframe(), its slot index) with one store round trip: tracker.py:29 reads the last
+        keyframe and tracker.py:101 writes it back at len(keyframes) - 1. Only the frontend appends keyframes
+        (main.py), so the index read with the keyframe is the one len() would return at the write-back. A
+        lock-guarded store (the reference's SharedKeyframes, frame.py:220-327: every Manager lock and Value access
+        is an IPC) is read under one lock hold: n_size once, then the slot, instead of last_keyframe()'s two n_size
+        reads plus a separate len()."""
+        kfs = self.keyframes
+        lock, n_size = getattr(kfs, "lock", None), getattr(kfs, "n_size", None)
+        if lock is not None and n_size is not None and hasattr(n_size, "value"):
+            with lock:
+                n = n_size.value
+                return (kfs[n - 1], n - 1) if n > 0 else (None, -1)
+        n = len(kfs)
+        return (kfs[n - 1], n - 1) if n > 0 else (None, -1)
 
     def _run_track(self, idx, valid, Xf, Cf, Nf, Qff, Xk, Ck, Nk, Qkf, T_WCf, T_WCk, use_calib, img_size, K,
                    fuse=None, direct=False, meas_k=None, valid_meas_k=None, max_iters=None):

@@ -121,3 +121,52 @@ def test_sharded_ba_protocol_gloo_world2(tmp_path):
     Tref, _, _ = O.gauss_newton("rays", Twc, Xs, Cs, ii, jj, idx, valid, Q, params, max_iter, 1e-8)
     np.testing.assert_allclose(T2[0], Tref, atol=1e-5)
     assert not np.array_equal(T2[0], Twc), "BA did not move the poses"
+
+
+class _StallShard:
+    """A shard whose factor schedule stalled on rank 1 only (HipShard.stalled() == M3S_ESTALL there)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.edge_sums = torch.zeros((4, ROW), dtype=torch.float64)
+
+    def linearize(self):
+        pass
+
+    def solve(self):
+        pass
+
+    def stalled(self):
+        return self.rank == 1
+
+
+def _stall_main(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from m3s.dist_ba import run_sharded
+
+        try:
+            run_sharded(_StallShard(rank), 3)
+            msg = "no error"
+        except RuntimeError as e:
+            msg = str(e)
+        # a collective after the failed solve: no rank is left waiting for another
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        with open(os.path.join(out_dir, f"stall_r{rank}.txt"), "w") as f:
+            f.write(f"{msg}|{t.item()}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_sharded_ba_stall_raises_on_every_rank(tmp_path):
+    """a stall on one rank (its loop stopped, its edge-sum rows zero) is a global decision: one MAX
+    all-reduce of the flag after the loop makes every rank raise M3S_ESTALL, and the ranks stay in step."""
+    mp.spawn(_stall_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        msg, tot = open(os.path.join(tmp_path, f"stall_r{r}.txt")).read().split("|")
+        assert "stall" in msg, f"rank {r}: {msg}"
+        assert float(tot) == 2.0

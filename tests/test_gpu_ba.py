@@ -401,3 +401,52 @@ def test_pack_fused_into_first_linearisation_is_bit_identical(mode, monkeypatch)
         monkeypatch.setenv("M3S_BA_FUSED_PACK", fused)
         out.append(_call(mode, G["Twc0"].numpy(), Xs, G["Cs"].numpy(), ii, jj, idx, valid, Q, K, 48, 66))
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.timeout(300)
+def test_sharded_hip_path_world2(tmp_path):
+    """the product's sharded BA (HipShard over libm3s.so + run_sharded) at N = 2. Two fresh
+    processes (gloo, both ranks on cuda:0, started before any GPU call in them: tests/sharded_child.py) each
+    linearise half of the 48-keyframe graph's edges into the shared (E, 36) fp64 edge-sum table, all-reduce it and
+    solve. Rays and calib, fresh and with record reuse (first call packs every shard edge, the second none): poses
+    and dx are bit-identical across ranks, between fresh and reuse, and to the unsharded gauss_newton_* (reference
+    call site global_opt.py:123-226)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK="0", OUT_DIR=str(tmp_path))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(repo, "tests", "sharded_child.py")],
+                                      env=env, cwd=repo, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        print(o[-2000:])
+        assert p.returncode == 0 and f"SHARDED_OK rank {r}" in o, o[-3000:]
+    R = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    E = int(R[0]["E"])
+    for mode in ("rays", "calib"):
+        for key in ("T", "dx"):
+            ref = R[0][f"{mode}_un_{key}"]
+            for r in range(2):
+                for v in ("", "_reuse0", "_reuse1"):
+                    got = R[r][f"{mode}{v}_{key}"]
+                    assert np.array_equal(got, ref), f"{mode}{v} {key} rank {r}: {np.abs(got - ref).max()}"
+        assert not np.array_equal(R[0][f"{mode}_T"], R[0]["Twc0"]), "BA did not move the poses"
+        # rank r packs only its own shard's edges on the first reuse call, none on the second
+        assert int(R[0][f"{mode}_reuse0_packed"]) + int(R[1][f"{mode}_reuse0_packed"]) == E
+        assert int(R[0][f"{mode}_reuse1_packed"]) == 0 and int(R[1][f"{mode}_reuse1_packed"]) == 0

@@ -284,13 +284,16 @@ def test_ba_symbolic_factorisation_matches_restatement(kind):
         assert got[0] < 0.1 * nb * (nb + 1) // 2 and got[1] < nb // 2
 
 
-def test_factor_graph_rejects_pin_other_than_one():
+def test_factor_graph_rejects_pin_above_one():
     """SURVEY.md §8 a-note 8: the C++ solvers fix exactly one pose (gn_kernels.cu:741,1157,1566) while the Python
-    write-back slices by cfg.pin (global_opt.py:125,161): any other pin is rejected before a solve starts."""
+    write-back slices by cfg.pin (global_opt.py:125,161): a pin above 1 would drop solved poses and is rejected before
+    a solve starts; pin = 0 is accepted (pose 0 is fixed in the solve either way)."""
     from m3s.global_opt import FactorGraph
 
     fg = FactorGraph(None, [], device="cpu")
-    for pin in (0, 2):
+    for pin in (0, 1):
+        assert FactorGraph._pin(dict(fg.cfg, pin=pin)) == pin
+    for pin in (2, 3):
         fg.cfg = dict(fg.cfg, pin=pin)
         for fn in (fg.solve_GN_rays, fg.solve_GN_calib):
             with pytest.raises(ValueError, match="pin"):
