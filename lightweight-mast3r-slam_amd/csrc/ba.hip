@@ -279,7 +279,16 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
     Ti[c] = a.Twc[ix * 8 + c];
     Tj[c] = a.Twc[jx * 8 + c];
   }
+#if BA_LIN_MATRIX
+  // T_ij in double (relSim3_d): in fp32 its translation t_j - t_i rounds at |t_i| (metres), an error coherent over
+  // every point of the edge (C4 EuRoC graph: 2.6e-6 -> 5e-7 from the fp64 truth, scripts/ba_prec_exp.py)
+  double Td[8];
+  relSim3_d(Ti, Tj, Td);
+#pragma unroll
+  for (int c = 0; c < 8; c++) Tij[c] = (float)Td[c];
+#else
   relSim3(Ti, Tj, Tij);
+#endif
 #if BA_LIN_MATRIX
   // the linear map of actSO3 (Y = X + 2w q x X + 2 q x (q x X), any |q|) times s, formed in fp64 once per block:
   // s (I + 2w[q]x + 2([q][q]^T - |q|^2 I)), kept as its difference from the identity, D = s R - I (Y = X + (D X + t)):
@@ -287,7 +296,7 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
   // than rounding s R itself (which put the ill-conditioned 6-KF fixtures at 1.6-1.8e-5 from the fp64 truth)
   float M[9];
   {
-    const double x = Tij[3], y = Tij[4], z = Tij[5], w = Tij[6], sc = Tij[7];
+    const double x = Td[3], y = Td[4], z = Td[5], w = Td[6], sc = Td[7];
     const double R[9] = {1.0 - 2.0 * (y * y + z * z), 2.0 * (x * y - z * w),       2.0 * (x * z + y * w),
                          2.0 * (x * y + z * w),       1.0 - 2.0 * (x * x + z * z), 2.0 * (y * z - x * w),
                          2.0 * (x * z - y * w),       2.0 * (y * z + x * w),       1.0 - 2.0 * (x * x + y * y)};
@@ -1466,7 +1475,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     float Tw[8], xi[7];
     for (int c = 0; c < 8; c++) Tw[c] = a.Twc[k * 8 + c];
     for (int c = 0; c < 7; c++) xi[c] = a.dx[(k - 1) * 7 + c];
-    retrSim3(xi, Tw);
+    retrSim3_d(xi, Tw);  // fp64 retraction (m3s_common.hpp: fp32 expSim3 cancels for small steps)
     for (int c = 0; c < 8; c++) a.Twc[k * 8 + c] = Tw[c];
   }
   n2 = wave_sum(n2);

@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(256) dense_finish_kernel(BaArgs a, int K, int 
     float T[8], xi[7];
     for (int c = 0; c < 8; c++) T[c] = a.Twc[k * 8 + c];
     for (int c = 0; c < 7; c++) xi[c] = a.dx[(k - 1) * 7 + c];
-    m3s::retrSim3(xi, T);
+    m3s::retrSim3_d(xi, T);  // fp64 retraction (m3s_common.hpp)
     for (int c = 0; c < 8; c++) a.Twc[k * 8 + c] = T[c];
   }
   n2 = wave_sum(n2);

@@ -146,6 +146,119 @@ __device__ __forceinline__ void retrSim3(const float* xi, float* T) {
   T[7] = D[7] * T[7];
 }
 
+// ---- fp64 forms of the global-BA pose math. The BA poses stay float (the reference's Twc), but
+// the two per-edge / per-pose steps whose fp32 rounding is coherent over a whole edge or pose run in double:
+//  * expSim3's series coefficients cancel catastrophically in fp32 for the small steps of a converging BA
+//    (C = (e^s - 1)/s, A = (1 - cos t)/t^2, B = (t - sin t)/t^3: relative errors up to O(1) at |phi| ~ 1e-2), and
+//  * relSim3's translation t_j - t_i rounds at |t_i| (metres), coherent over every point of the edge.
+// On the C4 EuRoC 320x512 K=256 rays graph (scripts/ba_prec_exp.py, an fp32-stage emulation of the HIP rows) the fp32
+// retraction alone put the poses 2.0e-5 from the fp64 truth; a double retraction 2.6e-6; plus a double relSim3 5e-7.
+// Same formulas and thresholds as the reference's float code (gn_kernels.cu:252-272, 299-413), evaluated in double
+// (what the fp64 truth, oracle/liboracle_m3s_f64.so, computes).
+__device__ __forceinline__ void quat_comp_d(const double* qi, const double* qj, double* out) {
+  out[0] = qi[3] * qj[0] + qi[0] * qj[3] + qi[1] * qj[2] - qi[2] * qj[1];
+  out[1] = qi[3] * qj[1] - qi[0] * qj[2] + qi[1] * qj[3] + qi[2] * qj[0];
+  out[2] = qi[3] * qj[2] + qi[0] * qj[1] - qi[1] * qj[0] + qi[2] * qj[3];
+  out[3] = qi[3] * qj[3] - qi[0] * qj[0] - qi[1] * qj[1] - qi[2] * qj[2];
+}
+
+__device__ __forceinline__ void actSO3_d(const double* q, const double* X, double* Y) {
+  const double uv0 = 2.0 * (q[1] * X[2] - q[2] * X[1]);
+  const double uv1 = 2.0 * (q[2] * X[0] - q[0] * X[2]);
+  const double uv2 = 2.0 * (q[0] * X[1] - q[1] * X[0]);
+  const double y0 = X[0] + q[3] * uv0 + (q[1] * uv2 - q[2] * uv1);
+  const double y1 = X[1] + q[3] * uv1 + (q[2] * uv0 - q[0] * uv2);
+  const double y2 = X[2] + q[3] * uv2 + (q[0] * uv1 - q[1] * uv0);
+  Y[0] = y0;
+  Y[1] = y1;
+  Y[2] = y2;
+}
+
+// T_ij = T_i^-1 T_j of two float poses, in double
+__device__ __forceinline__ void relSim3_d(const float* Ti, const float* Tj, double* Tij) {
+  const double si_inv = 1.0 / (double)Ti[7];
+  Tij[7] = si_inv * (double)Tj[7];
+  const double qi_inv[4] = {-(double)Ti[3], -(double)Ti[4], -(double)Ti[5], (double)Ti[6]};
+  const double qj[4] = {Tj[3], Tj[4], Tj[5], Tj[6]};
+  quat_comp_d(qi_inv, qj, &Tij[3]);
+  double t[3] = {(double)Tj[0] - (double)Ti[0], (double)Tj[1] - (double)Ti[1], (double)Tj[2] - (double)Ti[2]};
+  actSO3_d(qi_inv, t, t);
+  Tij[0] = t[0] * si_inv;
+  Tij[1] = t[1] * si_inv;
+  Tij[2] = t[2] * si_inv;
+}
+
+__device__ __forceinline__ void expSim3_d(const double* xi, double* T) {
+  const double tau[3] = {xi[0], xi[1], xi[2]};
+  const double phi[3] = {xi[3], xi[4], xi[5]};
+  const double sigma = xi[6];
+  const double scale = exp(sigma);
+  const double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  double imag, real;
+  if (theta_sq < 1e-6) {
+    const double theta_p4 = theta_sq * theta_sq;
+    imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_p4;
+    real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * theta_p4;
+  } else {
+    const double theta = sqrt(theta_sq);
+    imag = sin(0.5 * theta) / theta;
+    real = cos(0.5 * theta);
+  }
+  T[3] = imag * phi[0];
+  T[4] = imag * phi[1];
+  T[5] = imag * phi[2];
+  T[6] = real;
+  T[7] = scale;
+  const double theta = sqrt(theta_sq);
+  double A, B, C;
+  if (fabs(sigma) < 1e-6) {
+    C = 1.0;
+    if (fabs(theta) < 1e-6) {
+      A = 0.5;
+      B = 1.0 / 6.0;
+    } else {
+      A = (1.0 - cos(theta)) / theta_sq;
+      B = (theta - sin(theta)) / (theta_sq * theta);
+    }
+  } else {
+    C = (scale - 1.0) / sigma;
+    if (fabs(theta) < 1e-6) {
+      const double sigma_sq = sigma * sigma;
+      A = ((sigma - 1.0) * scale + 1.0) / sigma_sq;
+      B = (scale * 0.5 * sigma_sq + scale - 1.0 - sigma * scale) / (sigma_sq * sigma);
+    } else {
+      const double a = scale * sin(theta);
+      const double b = scale * cos(theta);
+      const double c = theta_sq + sigma * sigma;
+      A = (a * sigma + (1.0 - b) * theta) / (theta * c);
+      B = (C - ((b - 1.0) * sigma + a * theta) / c) / theta_sq;
+    }
+  }
+  const double c0 = phi[1] * tau[2] - phi[2] * tau[1];
+  const double c1 = phi[2] * tau[0] - phi[0] * tau[2];
+  const double c2 = phi[0] * tau[1] - phi[1] * tau[0];
+  const double d0 = phi[1] * c2 - phi[2] * c1;
+  const double d1 = phi[2] * c0 - phi[0] * c2;
+  const double d2 = phi[0] * c1 - phi[1] * c0;
+  T[0] = C * tau[0] + A * c0 + B * d0;
+  T[1] = C * tau[1] + A * c1 + B * d1;
+  T[2] = C * tau[2] + A * c2 + B * d2;
+}
+
+// T <- Exp(xi) * T of a float pose and a float step, in double, rounded back to float once
+__device__ __forceinline__ void retrSim3_d(const float* xi, float* T) {
+  double x[7], D[8], Td[8];
+  for (int c = 0; c < 7; c++) x[c] = xi[c];
+  for (int c = 0; c < 8; c++) Td[c] = T[c];
+  expSim3_d(x, D);
+  double q1[4], t1[3];
+  quat_comp_d(&D[3], &Td[3], q1);
+  actSO3_d(&D[3], &Td[0], t1);
+  for (int c = 0; c < 3; c++) T[c] = (float)(t1[c] * D[7] + D[c]);
+  for (int c = 0; c < 4; c++) T[3 + c] = (float)q1[c];
+  T[7] = (float)(D[7] * Td[7]);
+}
+
 // ---- wave64 reductions (DPP/permute through __shfl_xor; no warp-synchronous assumptions) ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

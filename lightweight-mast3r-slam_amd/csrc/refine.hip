@@ -243,8 +243,9 @@ __device__ __forceinline__ void exact_survivors(const h1* __restrict__ img, int 
 // lds_addr: the row's LDS byte address (wave-uniform)
 __device__ __forceinline__ void lds_dma_row(const h1* g, unsigned lds_addr) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  // m0 is clobbered: the compiler sets it itself for its own global_load_lds, and must not keep a value live across this
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(g) : "memory", "m0");
+  // M0 is an operand ({m0}): the compiler writes it itself right before the asm and knows its value (it also sets M0
+  // for its own global_load_lds); the s_nop is the wait state between that M0 write and the DMA that reads it
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
 
 // the packed window's variant: the survivors' three chunks are read from the resident LDS planes (base = candidate

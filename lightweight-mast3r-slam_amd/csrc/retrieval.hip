@@ -176,9 +176,8 @@ rq_gemm_topk_kernel(const uint4* __restrict__ cfrag, const float* __restrict__ c
       const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(rq_lptr)&dst[i * 64]);
       // one wait state between the M0 write and the LDS DMA that reads it (CDNA3/4 manually inserted wait states;
       // the compiler's own global_load_lds sequences keep one instruction there)
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0),
-                   "v"(qa + (size_t)s * RQ_QU + i * 64)
-                   : "memory", "m0");  // m0 clobbered: the compiler must not keep its own M0 value live across it
+      asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(qa + (size_t)s * RQ_QU + i * 64), "{m0}"(m0)
+                   : "memory");  // M0 an operand: the compiler writes it before the asm and knows its value
     }
   };
   // codebook: global -> VGPR two k-steps ahead (a 3-slot register ring), by inline-asm loads the compiler does

@@ -277,9 +277,10 @@ def test_ba_k256_front_phase_matches_group_schedules(chess_graph, monkeypatch):
 # The timed BA workloads at their full keyframe resolution (main.py:150-155 solves at the keyframes' own size):
 # C5 = 7-Scenes chess, 384x512 calib; the ETH3D half of C5 = 304x512 calib (ETH3D ground truth is not in the
 # reference, so the chess trajectory carries the ETH3D image shape); C4 = EuRoC MH_02, 320x512 rays. 2 GN iterations
-# with the early exit off, against the oracle's fp64 truth (the checker only) at SURVEY a-note 6's 1e-5 — or, where
-# fp32 rows cannot reach it (C4), within twice the error of the fp32-row restatement. Every edge then spans ~8
-# linearisation chunks of 24,576 points, the bench's exact chunking.
+# with the early exit off, against the oracle's fp64 truth (the checker only) at SURVEY a-note 6's 1e-5. C4 needed the
+# fp64 retraction and relative pose (m3s_common.hpp retrSim3_d / relSim3_d): with the reference's fp32 forms it sat
+# at 2.45e-5 (scripts/ba_prec_exp.py). Every edge then spans ~8 linearisation chunks of 24,576 points, the bench's
+# exact chunking.
 FULL_CASES = [("C5-chess", "chess", 384, 512, "calib"), ("C5-eth3d", "chess", 304, 512, "calib"),
               ("C4-euroc", "euroc", 320, 512, "rays")]
 
@@ -320,16 +321,5 @@ def test_ba_k256_full_resolution_vs_fp64_truth(case, traj, H, W, mode):
     print(f"{case} K=256 {H}x{W} {mode}, {h['ii'].shape[0]} edges, {iters} iterations: pose err vs fp64 truth "
           f"{err:.2e}, dx err {derr:.2e}")
     assert dx.shape == (255, 7)
-    if max(err, derr) > 1e-5:
-        # The fp32 rows themselves cost more than 1e-5 on this graph: the restatement with the reference's fp32
-        # per-point arithmetic and fp64 sums (the oracle) lands farther than 1e-5 from the truth too, and the
-        # reference's own fp32 sum order (oracle set_ref_order, gn_kernels.cu:36-55) 8x farther than this build
-        # (C4: 2.0e-4 pose / 1.3e-3 dx). The bound is then twice the fp32-row restatement's error.
-        T32, dx32, _ = O.gauss_newton(mode, *args, iters, 0.0)
-        e32, d32 = np.abs(T32 - T_ref).max(), np.abs(dx32 - dx_ref).max()
-        print(f"  fp32-row restatement (fp64 sums) vs fp64 truth: pose {e32:.2e}, dx {d32:.2e}")
-        assert e32 > 1e-5 or d32 > 1e-5, "the fp32-row restatement meets 1e-5 here: so must the HIP build"
-        assert err <= 2 * max(e32, 1e-5) and derr <= 2 * max(d32, 1e-5)
-    else:
-        np.testing.assert_allclose(T, T_ref, atol=1e-5)
-        np.testing.assert_allclose(dx, dx_ref, atol=1e-5)
+    np.testing.assert_allclose(T, T_ref, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(dx, dx_ref, rtol=0, atol=1e-5)
