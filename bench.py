@@ -309,10 +309,10 @@ BA_SUM_BYTES = 36 * 8
 def ba_plan_info(lib, plan):
     from m3s import _lib
 
-    info = (ctypes.c_int * 10)()
+    info = (ctypes.c_int * 12)()
     _lib.check(lib.m3s_ba_plan_info(ctypes.byref(plan), info))
     keys = ("chunks", "factor_blocks", "levels", "wide_steps", "dense", "targets", "edges", "poses", "subtree_steps",
-            "subtree_workgroups")
+            "subtree_workgroups", "supernodes", "supernode_workgroups")
     return dict(zip(keys, list(info)))
 
 

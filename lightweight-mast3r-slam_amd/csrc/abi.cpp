@@ -557,7 +557,7 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_SYM_SECTIONS = 19;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_SYM_SECTIONS = 20;  // the symbolic half's sections (build_symbolic)
 constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
 constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
 constexpr int BA_SP_PLAN_BYTES = 144 * 1024;  // ba.hip SP_PLAN_BYTES: LDS of the one-workgroup factor kernel
@@ -568,6 +568,13 @@ constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 inline size_t ba_max_pairs(int Kp) {
   const size_t nb = (size_t)std::max(0, Kp - 1);
   return std::min(nb * nb * nb / 6 + nb * nb + 64, 32 * ba_max_blocks(Kp) + 64);
+}
+// ints reserved for the supernodal plan (ba_snode_plan): records, rows, blk maps, children and lists per supernode,
+// and per pull its map (a pull per off-diagonal factor block at most, R <= 36 rows each); a plan that needs more
+// falls back to the column-task solver
+inline size_t ba_sn_capacity(int Kp) {
+  const size_t nb = (size_t)std::max(0, Kp - 1);
+  return 1024 + 64 * nb + 8 * ba_max_blocks(Kp);
 }
 size_t ba_blob_capacity(int Kp, int E, int chunks) {
   const size_t nb = (size_t)std::max(0, Kp - 1), nLm = ba_max_blocks(Kp);
@@ -583,7 +590,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       // U tasks), sources and their maps (each update pair once), slot and column maps; apply table
                       (size_t)nb * (4 + 16 + 2 * (BA_MAX_WIDE_STEPS + 1) + 4) + 8 * (nb + 2 * nLm) + 4 * nLm +
                       ba_max_pairs(Kp) + nLm + nb + 8 * (size_t)nb + nLm +
-                      2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm);  // + the dataflow schedule
+                      2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm) +  // + the dataflow schedule
+                      ba_sn_capacity(Kp);                                    // + the supernodal plan
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -727,6 +735,7 @@ struct PlanSym {
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
   int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
   int front_cut = 0, front_wgs = 0, front_napply = 0;  // frontal subtree phase (ba_front_kernel), see build_symbolic
+  int snode = 0, sn_wgs = 0, nsn = 0;  // supernodal factorisation (ba_snode_kernel): its bottom workgroups, supernodes
   bool pack_deferred = false;    // the plan's pack runs inside its first linearisation (set at plan time, under g_sym_mu)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
@@ -750,9 +759,27 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   // factorisation costs ~3.8 us per elimination-tree level plus ~0.03 us per source-map entry (its
   // update volume); the dense one ~2.7 us per pose (its pivot chain)
   Y->dense = has_dense && 3.8 * S.nlev + 0.03 * (double)S.sidx.size() > 2.7 * S.nb;
-  if (const char* f = getenv("M3S_BA_SOLVER")) {  // tests and experiments: force one factorisation
-    if (!strcmp(f, "sparse")) Y->dense = 0;
-    if (!strcmp(f, "dense") && has_dense) Y->dense = 1;
+  const char* solver = getenv("M3S_BA_SOLVER");
+  if (solver) {  // tests and experiments: force one factorisation
+    if (!strcmp(solver, "sparse") || !strcmp(solver, "snode")) Y->dense = 0;
+    if (!strcmp(solver, "dense") && has_dense) Y->dense = 1;
+  }
+  // supernodal factorisation (ba_snode.cpp / ba_snode.hip): M3S_BA_SOLVER=snode; its back substitution runs in the
+  // one-workgroup kernel on a schedule without factor tasks. M3S_BA_SN_CUT forces the supernodal tree's cut height.
+  std::vector<int> sntab;
+  if (!Y->dense && solver && !strcmp(solver, "snode")) {
+    const char* ce = getenv("M3S_BA_SN_CUT");
+    int nwg = 0;
+    double est = 0.0;
+    const int nsn = ba_snode_plan(S, M3S_BA_SN_SMAX, M3S_BA_SN_GROUPS, 64 * 4, ce && *ce ? atoi(ce) : -1, &sntab, &nwg,
+                                  &est);
+    if (nsn > 0 && sntab.size() <= ba_sn_capacity(Kp)) {
+      Y->snode = 1;
+      Y->sn_wgs = nwg;
+      Y->nsn = nsn;
+    } else {
+      sntab.clear();
+    }
   }
   // the leaf end of the elimination tree: by default the subtree phase below (one launch); with M3S_BA_WIDE or
   // M3S_BA_FLOW=0 the earlier split into multi-workgroup launches (steps [0, wide_steps)), the root end in the
@@ -800,7 +827,9 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   };
   const char* senv = getenv("M3S_BA_SUB");
   if (senv != nullptr && *senv == '\0') senv = nullptr;
-  if (const char* w = getenv("M3S_BA_WIDE")) {
+  if (Y->snode) {
+    Y->wide_steps = 0;  // the supernodal kernels factor everything
+  } else if (const char* w = getenv("M3S_BA_WIDE")) {
     const int thr = atoi(w);
     int last = -1;
     for (int l = 0; l <= S.nlev; l++)
@@ -848,7 +877,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   std::vector<int> fronttab, frontapply;
   const char* fenv2 = getenv("M3S_BA_FRONT");
   const int front_forced = fenv2 && *fenv2 ? atoi(fenv2) : 0;
-  if (front_forced != 0 && !Y->dense && Y->sub_cut == 0 && Y->wide_steps >= 2 && S.nlev >= 2) {
+  if (front_forced != 0 && !Y->dense && !Y->snode && Y->sub_cut == 0 && Y->wide_steps >= 2 && S.nlev >= 2) {
     const int hi = std::min(Y->wide_steps - 1, S.nlev - 1);
     const size_t u_cap = (ba_max_blocks(Kp) - (size_t)S.nL) * 64;
     for (int cut = front_forced > 0 ? std::min(front_forced, hi) : hi; cut >= 1; cut--) {
@@ -893,11 +922,16 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     }
   }
   // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
-  if (flow_on) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
+  // (supernodal: a schedule of the back substitution alone, every column factored before the kernel starts)
+  if (flow_on || Y->snode) ba_flow_schedule(S, Y->snode ? S.nlev + 1 : Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
   Y->flow = sched.empty() ? 0 : 1;
   if (Y->flow && !flow_fits(sched)) {  // the kernel would run level-synchronously: drop the schedule (and say so)
     Y->flow = 0;
     sched.clear();
+  }
+  if (Y->snode && !Y->flow) {  // the back substitution after the supernodal factor needs the dataflow kernel
+    Y->err = "ba: the supernodal solver needs the back-substitution schedule in LDS";
+    return M3S_EINVAL;
   }
   if (!Y->flow && Y->sub_cut > 0) {  // the subtree phase needs the dataflow kernel (it runs the subtrees' spine groups)
     Y->err = "ba: the subtree phase needs the dataflow schedule";
@@ -906,7 +940,7 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
                                                    &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
                                                    &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
-                                                   &step_rec, &subtab,  &fronttab,  &frontapply};
+                                                   &step_rec, &subtab,  &fronttab,  &frontapply, &sntab};
   size_t total = 0;
   for (int k = 0; k < BA_SYM_SECTIONS; k++) {
     Y->off[k] = total;
@@ -988,7 +1022,7 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
       (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
       (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
       (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec,
-      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply};
+      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply, (const void**)&a.sn_tab};
   for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
@@ -1002,6 +1036,8 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   a.front_wgs = Y->front_wgs;
   a.front_napply = Y->front_napply;
   a.front_u = a.L + (size_t)Y->nL * 64;
+  a.snode = Y->snode;
+  a.sn_wgs = Y->sn_wgs;
   return a;
 }
 
@@ -1428,6 +1464,8 @@ extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   info[7] = P->Kp;
   info[8] = Y->front_wgs > 0 ? Y->front_cut : Y->sub_cut;
   info[9] = Y->front_wgs > 0 ? Y->front_wgs : Y->sub_wgs;
+  info[10] = Y->snode ? Y->nsn : 0;
+  info[11] = Y->snode ? Y->sn_wgs : 0;
   return M3S_OK;
 }
 

@@ -1460,8 +1460,10 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   __syncthreads();
   SPST(3 + 2 * nlev);
-  const bool failed = s_bad != 0 || ((a.wide_steps > 0 || a.sub_wgs > 0) && *a.bad != 0);
-  const bool stalled = (s_bad & BA_BAD_STALL) != 0;
+  // the multi-workgroup factor launches (wide steps, subtree phase, supernodal kernels) report through *a.bad
+  const int ext_bad = (a.wide_steps > 0 || a.sub_wgs > 0 || a.snode) ? *(volatile int*)a.bad : 0;
+  const bool failed = s_bad != 0 || ext_bad != 0;
+  const bool stalled = ((s_bad | ext_bad) & BA_BAD_STALL) != 0;
   const int n = a.nb * 7;
   float n2 = 0.0f;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -1550,9 +1552,21 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 // assembly (nL factor blocks + nb rhs rows), then the one-workgroup factor / solve / retraction
 // step_tasks / step_base / step_na: per wide step its tasks, its first task record, its factor tasks (the rest are
 // update groups)
+extern "C" hipError_t m3s_launch_ba_snode(const BaArgs* a, int nwg, hipStream_t s);
+
 extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, const int* step_tasks,
                                           const int* step_base, const int* step_na, hipStream_t s) {
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
+  if (a->snode) {  // supernodal factor (ba_snode.hip), then the back substitution + retraction on a factor-free schedule
+    const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 + (size_t)a->nb * 12;
+    if (!a->flow || lds > (size_t)m3s::SP_PLAN_BYTES) return hipErrorInvalidValue;
+    if (a->nb > 0) {
+      const hipError_t e = m3s_launch_ba_snode(a, a->sn_wgs, s);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+    return hipGetLastError();
+  }
   static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
   static_assert(m3s::FRONT_LDS_BYTES == 159 * 1024, "abi.cpp BA_FRONT_LDS_BYTES");
   // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column

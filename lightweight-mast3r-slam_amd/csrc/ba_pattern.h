@@ -97,3 +97,20 @@ int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vec
 // number of workgroups (0: the cut does not fit); *u_doubles = the scratch size, *napply = the apply entries.
 int ba_front_plan(const BaPattern& P, int cut, size_t lds_bytes, std::vector<int>* tab, std::vector<int>* apply,
                   size_t* u_doubles, int* napply);
+
+// Supernodal factorisation (ba_snode.hip, ba_snode.cpp): chains of consecutive etree columns as supernodes of at most
+// `smax` columns, each a dense register panel of one group of 4 waves (7 rows per block row + the rhs row, at most
+// `max_rows` rows), left-looking pulls from every descendant column, the supernodal tree cut at a height (cut_req >= 0
+// forces it, -1 picks the estimate's best): the subtrees below in a multi-workgroup launch, the rest in one
+// workgroup; `groups` groups per workgroup walk list-scheduled supernode lists. Layout (ints):
+//   [16-int header: nsn, nwg (bottom workgroups), off_rec, off_pull, off_lists, cut height, groups, smax, max pairs,
+//    tree height]
+//   [records 8 ints per supernode: {s, R, rows offset, blk offset, pull begin, pull end, child begin, child end}]
+//   per supernode: rows (R block rows: its columns, then the rows below), blk (s x R: factor block of L(row ib,
+//   column t) or -1), children, per pull its map (R: block of L(row ib, k) or -1)
+//   [pulls: 2 ints {k, map offset}]
+//   [lists: (nwg + 1) x (groups + 1) item offsets: workgroup w < nwg bottom, w = nwg the top one] [items]
+// Offsets are absolute (ints from the table start). Returns the number of supernodes (0: a panel does not fit or the
+// pattern breaks the row-subset property: use another solver); *cost_us = the estimated makespan.
+int ba_snode_plan(const BaPattern& P, int smax, int groups, int max_rows, int cut_req, std::vector<int>* tab,
+                  int* nwg, double* cost_us);

@@ -7,6 +7,13 @@
 #define BA_MODE_RAYS 1
 #define BA_MODE_CALIB 2
 
+#ifndef M3S_BA_SN_GROUPS  // supernodal factorisation (ba_snode.hip): groups of 4 waves per workgroup, columns per supernode
+#define M3S_BA_SN_GROUPS 2
+#endif
+#ifndef M3S_BA_SN_SMAX
+#define M3S_BA_SN_SMAX 4
+#endif
+
 #ifndef M3S_BA_SP_WAVES
 #define M3S_BA_SP_WAVES 16  // waves of the one-workgroup sparse factorisation (ba.hip) and of its cost model (abi.cpp)
 #endif
@@ -95,6 +102,9 @@ struct BaArgs {
   int* done;   // early-exit flag (|dx| < delta_thresh)
   int* iters;  // iterations executed
   int* bad;    // non-positive pivot seen by a multi-workgroup factor step (cleared by the assembly)
+  const int* sn_tab;  // supernodal factorisation (ba_pattern.h ba_snode_plan), or null
+  int snode;          // the factor ran in ba_snode_kernel (the factor kernel then only substitutes back)
+  int sn_wgs;         // its multi-workgroup launch's workgroups
   int* stalled;  // sticky: a dataflow / LDS hand-off wait timed out in some solve of this plan (M3S_ESTALL)
   int force_stall;  // tests only (M3S_BA_FORCE_STALL): the dataflow waits are never satisfied
 };
