@@ -94,3 +94,39 @@ def test_front_phase_on_trajectory_graphs(front_checker, tmp_path, traj, cut):
     f.write_text("".join(f"{a} {b}\n" for a, b in zip(G["ii"].tolist(), G["jj"].tolist())))
     out = subprocess.run([front_checker, "-f", str(f), str(cut)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("OK") and " nwg 0 " not in out.stdout, out.stdout + out.stderr
+
+
+@pytest.fixture(scope="module")
+def snode_checker(tmp_path_factory):
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    exe = str(tmp_path_factory.mktemp("snode") / "ba_snode_check")
+    subprocess.check_call([cxx, "-O2", "-std=c++17", "-I", CSRC, os.path.join(REPO, "scripts", "ba_snode_check.cpp"),
+                           os.path.join(CSRC, "ba_pattern.cpp"), os.path.join(CSRC, "ba_snode.cpp"), "-o", exe])
+    return exe
+
+
+def test_snode_plan_random_graphs(snode_checker):
+    """The supernodal plan (csrc/ba_snode.cpp) interpreted with ba_snode_kernel's arithmetic and wait rules
+    (scripts/ba_snode_check.cpp) on random trajectory-like graphs, smax 1..6, cost-model and forced cuts: every
+    workgroup list drains (no deadlock) and factor + forward substitution equal a dense Cholesky to 1e-9."""
+    out = subprocess.run([snode_checker], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.count("rel err") >= 8, out.stdout
+
+
+@pytest.mark.parametrize("traj", ["chess", "euroc"])
+def test_snode_plan_trajectory_graphs(snode_checker, tmp_path, traj):
+    """The C5 / C4 trajectory graphs (K = 256): every cut (all top, cost model, all bottom) and smax 1, 2, 4, 6."""
+    import sys
+
+    sys.path.insert(0, os.path.join(REPO, "lightweight-mast3r-slam_amd"))
+    from m3s.synthetic import chess_poses, euroc_poses, make_traj_graph
+
+    G = make_traj_graph((chess_poses if traj == "chess" else euroc_poses)(256), 24, 32, seed=1)
+    f = tmp_path / "edges.txt"
+    f.write_text("".join(f"{a} {b}\n" for a, b in zip(G["ii"].tolist(), G["jj"].tolist())))
+    out = subprocess.run([snode_checker, str(f)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.count("rel err") == 8, out.stdout
