@@ -649,9 +649,10 @@ __global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h
       s_red[t.wid][2] = na;
     }
     __syncthreads();
+    // block-uniform: SGPRs (readfirstlane), not VGPRs live across every level
     const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
-    t.fu = (s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall;
-    t.fv = (s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall;
+    t.fu = __builtin_amdgcn_readfirstlane((s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall);
+    t.fv = __builtin_amdgcn_readfirstlane((s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall);
     t.tcu = tx * RT_TW + RT_TW / 2 + t.fu;
     t.tcv = ty * RT_TH + RT_TH / 2 + t.fv;
   }
@@ -670,19 +671,22 @@ __global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h
   if (threadIdx.x == 0 && blockIdx.x < 8192) g_refine_bstamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
   h1 max_score = (h1)0.0f;   // numeric_limits<c10::Half>::min() == +0, never reset between levels
-  for (int d = dilation_max; d > 0; d--) {
-    const bool first = d == dilation_max;
-    switch (d) {
-      case 8: refine_level<8, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 7: refine_level<7, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 6: refine_level<6, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 5: refine_level<5, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 4: refine_level<4, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 3: refine_level<3, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      case 2: refine_level<2, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-      default: refine_level<1, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, first); break;
-    }
-  }
+  // the levels as straight-line code (d = dilation_max .. 1) instead of a loop over a switch of the eight inlined level
+  // bodies: across that loop's back edge the register allocator made ~800 copies and spilled 19 VGPRs (80 B of scratch
+  // per lane, ~18 MB of scratch writes per frame); straight-line, the screened kernel takes 118 VGPRs and spills none
+  // (csrc/Makefile checks it: scripts/isa_check_spills.py)
+#define RT_LEVEL(DD)                                                                                        \
+  if (dilation_max >= DD)                                                                                   \
+    refine_level<DD, SCREEN, LIN_OUT>(t, active, q, cu, cv, max_score, lds, s_red, dilation_max == DD);
+  RT_LEVEL(8)
+  RT_LEVEL(7)
+  RT_LEVEL(6)
+  RT_LEVEL(5)
+  RT_LEVEL(4)
+  RT_LEVEL(3)
+  RT_LEVEL(2)
+  RT_LEVEL(1)
+#undef RT_LEVEL
   if (mine && active) store_out<LIN_OUT>(outv, bn, W, cu, cv);
 #ifdef M3S_REFINE_BSTAMPS
   const unsigned long long nact = __popcll(__ballot(active));
