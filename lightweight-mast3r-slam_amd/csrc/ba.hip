@@ -602,10 +602,18 @@ __global__ void __launch_bounds__(64) ba_edge_kernel(BaArgs a, BaParams p, int E
 // dx = -x in pose order (0 on a failed pivot: the reference's silent zero step), the Sim(3) retraction
 // and the |dx| early exit.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL) {
+__device__ __forceinline__ void ba_assemble_one(const BaArgs& a, int nL, int b, int t);
+
+// xcd_stride 8: only the blocks dispatched to XCD 0 work, each on items b / 8, b / 8 + nwork, ... (the factor steps and
+// the one-workgroup kernel then read the assembled blocks from that XCD's L2)
+__global__ void __launch_bounds__(64) ba_assemble_kernel(BaArgs a, int nL, int xcd_stride) {
   if (*a.done) return;
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
+  if (xcd_stride > 1 && blockIdx.x % xcd_stride != 0) return;
+  const int nwork = gridDim.x / xcd_stride;
+  for (int b = blockIdx.x / xcd_stride; b < nL + a.nb; b += nwork) ba_assemble_one(a, nL, b, threadIdx.x);
+}
+
+__device__ __forceinline__ void ba_assemble_one(const BaArgs& a, int nL, int b, int t) {
   if (b == 0 && t == 0) *a.bad = 0;  // the multi-workgroup factor steps of this solve start clean
   const int* ptr = b < nL ? a.asm_ptr + b : a.rhs_ptr + (b - nL);
   const int* ent = b < nL ? a.asm_ent : a.rhs_ent;
@@ -1116,10 +1124,13 @@ __device__ __forceinline__ void sp_back_column_flow(const BaArgs& a, const SpTab
 // Each task reads one 32-B record built with the plan ({j, b0, b1, pull group} and the group's source range), in
 // the same round trip as the early-exit flag: the level / column / group table lookups that used to precede the
 // column's own loads (four dependent global round trips) are gone.
-__global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int rec_base, int na) {
+__global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int rec_base, int na, int xcd_stride) {
   __shared__ double s_red[64];
   const int lane = threadIdx.x;
-  const int task = blockIdx.x;
+  // xcd_stride 8 (M3S_BA_XCD0, default): only the blocks dispatched to XCD 0 (blockIdx % 8 == 0) work, so every
+  // step and the one-workgroup kernel share one XCD's L2
+  if (xcd_stride > 1 && blockIdx.x % xcd_stride != 0) return;
+  const int task = blockIdx.x / xcd_stride;
   const int4 r0 = a.step_rec[2 * (rec_base + task)], r1 = a.step_rec[2 * (rec_base + task) + 1];
   if (*a.done) return;
   const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
@@ -1554,9 +1565,23 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 // update groups)
 extern "C" hipError_t m3s_launch_ba_snode(const BaArgs* a, int nwg, hipStream_t s);
 
+// XCD affinity of the solve (M3S_BA_XCD0, default on): every multi-workgroup factor step and the one-workgroup kernel
+// (block 0) run on XCD 0, so each step reads the previous one's blocks from that XCD's L2 instead of across the
+// fabric. Measured (scripts/gpu_r05_xcd.sh, same box, two pairs): solve C5 0.393 -> 0.375 ms, C4 0.424 -> 0.409 ms.
+static int ba_xcd_stride() {
+  static const int xs = [] {
+    const char* e = getenv("M3S_BA_XCD0");
+    return (e && atoi(e) == 0) ? 1 : 8;
+  }();
+  return xs;
+}
+
 extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float delta_thresh, const int* step_tasks,
                                           const int* step_base, const int* step_na, hipStream_t s) {
-  if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL);
+  const int xs = ba_xcd_stride();
+  // the assembly stays spread over every XCD: pinned to XCD 0 (32 CUs, item-strided) it took longer than the L2 reads
+  // it saved the first step (solve C5 0.381 vs 0.375 ms)
+  if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL, 1);
   if (a->snode) {  // supernodal factor (ba_snode.hip), then the back substitution + retraction on a factor-free schedule
     const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 + (size_t)a->nb * 12;
     if (!a->flow || lds > (size_t)m3s::SP_PLAN_BYTES) return hipErrorInvalidValue;
@@ -1584,8 +1609,8 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
   }
   for (int l = a->front_wgs > 0 ? a->front_cut : 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0)
-      hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l]), dim3(64), 0, s, *a, step_base[l],
-                         step_na[l]);
+      hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l] * xs), dim3(64), 0, s, *a, step_base[l],
+                         step_na[l], xs);
   if (flow_fits)
     hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else if (lds <= (size_t)m3s::SP_PLAN_BYTES) {
