@@ -40,8 +40,12 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // them; ~45% of the FMAs in rays mode). Products and sums in fp32 (packed: two points per instruction) over
 // runs of BA_RUN_LEN rounds per slot, each run then added to the fp64 accumulators (the kernel is VALU-issue
 // bound; fp64 products put no measurable accuracy gain against the fp64 truth once runs are short).
-#ifndef BA_RUN_LEN  // rounds per fp32 run (points per slot): 8 -> 16 took C5 2.25 -> 2.19 ms, C4 1.91 -> 1.83 ms;
-#define BA_RUN_LEN 16  // the 48-round full-chunk graphs stay within 1e-5 of the fp64 truth
+#ifndef BA_RUN_LEN  // rounds per fp32 run (points per slot): 8 -> 16 took C5 2.25 -> 2.19 ms, C4 1.91 -> 1.83 ms.
+// Round 5: 64 (a chunk is <= 48 rounds, so one fp32 run per slot and chunk, flushed once): with the fp64 retraction and
+// relative pose (m3s_common.hpp) the fp32 runs no longer carry the error budget: every BA fixture <= 3.5e-6 from the
+// fp64 truth (16: <= 7.2e-6; scripts/ba_acc.py), linearisation -2 % (C5 2.28 -> 2.22 ms, C4 1.86 -> 1.82 ms in
+// scripts/ba_exp.py spans; profiles/r05_ba_runlen.txt)
+#define BA_RUN_LEN 64
 #endif
 template <unsigned MASK>
 __device__ __forceinline__ void acc_local_f2(f2* L, f2* v, const f2 J[7], f2 w, f2 e) {
