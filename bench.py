@@ -295,13 +295,14 @@ BA_LEGS = {"C5": dict(traj="chess", mode="calib", H=384, W=512), "C4": dict(traj
            "C5e": dict(traj="chess", mode="calib", H=304, W=512)}
 BA_PMC_TAG = {"C5": "_ba", "C4": "_ba_c4", "C5e": "_ba_eth3d"}
 # Compulsory HBM bytes of the build's BA loop. Once per call the pack streams, per point and edge,
-# valid 1 + idx 8 + Q 4 in and the 16-B record out (29 B), and gathers from the keyframes' X (12 B) and C (4 B),
-# compulsory once per keyframe point. Every GN iteration then streams only the 16-B record of each point of each
-# edge and the 12-B X_j of each point of each distinct target keyframe (the edges of one target share that slab in
-# L2), plus per edge its chunk partials (36 doubles written by ba_lin, read back by ba_edge) and its edge-sum row.
-BA_PACK_EDGE_BYTES = 29
+# valid 1 + idx 8 + Q 4 in and the record out, and gathers from the keyframes' X (12 B) and C (4 B), compulsory once
+# per keyframe point. Every GN iteration then streams only the record of each point of each edge and the 12-B X_j of
+# each point of each distinct target keyframe (the edges of one target share that slab in L2), plus per edge its
+# chunk partials (36 doubles written by ba_lin, read back by ba_edge) and its edge-sum row. Records (ba.hip
+# pack_record): calib 12 B {u | v << 16, log z_i, sw}, points 16 B {X_i, sw}, rays 16 B {X_i / |X_i|, sw} + 4 B |X_i|.
+BA_PACK_IN_BYTES = 13
 BA_PACK_KF_BYTES = 16
-BA_REC_BYTES = 16
+BA_REC_BYTES = {"calib": 12, "points": 16, "rays": 20}
 BA_XJ_BYTES = 12
 BA_SUM_BYTES = 36 * 8
 
@@ -377,7 +378,7 @@ def bench_ba(args, rank, world, dev, leg):
     # roofline of the dominant kernel (the linearisation) at the build's compulsory bytes per iteration
     lin_s = spans["ba_linearize"] * 1e-3
     n_e = e1 - e0
-    rec_bytes = BA_REC_BYTES + (4 if mode == "rays" else 0)  # rays: + |Xi| (the record holds the unit ray)
+    rec_bytes = BA_REC_BYTES[mode]
     alg = n_e * N * rec_bytes + info["targets"] * N * BA_XJ_BYTES + n_e * (2 * info["chunks"] + 1) * BA_SUM_BYTES
     pmc = pmc_entry(f"ba_lin_kernel<{1 if mode == 'rays' else 2}, false>", pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     traffic = pmc["traffic_bytes"] if pmc else None
@@ -431,7 +432,7 @@ def bench_ba(args, rank, world, dev, leg):
     # the pack's cost: its own launch, or what it adds to the first linearisation when fused into it
     ms_pack = spans["ba_lin_pack"] - spans["ba_linearize"] if fused else spans["ba_pack"]
     pack_s = (spans["ba_lin_pack"] if fused else spans["ba_pack"]) * 1e-3
-    pack_bytes = n_e * N * (BA_PACK_EDGE_BYTES + (4 if mode == "rays" else 0)) + args.ba_kf * N * BA_PACK_KF_BYTES
+    pack_bytes = n_e * N * (BA_PACK_IN_BYTES + rec_bytes) + args.ba_kf * N * BA_PACK_KF_BYTES
     pack_pmc = pmc_entry(f"ba_pack_kernel<{1 if mode == 'rays' else 2}>",
                          pattern=f"r[0-9][0-9]{BA_PMC_TAG[leg]}_pmc.json")
     out = {"edges_per_s": E * args.ba_iters / el, "n_gpus": world, "keyframes": args.ba_kf, "edges_dir": E,
@@ -448,7 +449,7 @@ def bench_ba(args, rank, world, dev, leg):
                     "frac": (pack_bytes + (alg if fused else 0)) / pack_s / 1e9 / HBM_PEAK_GBS,
                     "bytes": pack_bytes, "fused_into_first_linearisation": fused,
                     "traffic": None if fused else (pack_pmc["traffic_bytes"] if pack_pmc else None),
-                    "note": f"once per call: {BA_PACK_EDGE_BYTES} B per point and edge + {BA_PACK_KF_BYTES} B per "
+                    "note": f"once per call: {BA_PACK_IN_BYTES + rec_bytes} B per point and edge + {BA_PACK_KF_BYTES} B per "
                             f"keyframe point (compulsory)" + ("; fused into the first linearisation (ba_lin_kernel"
                             "<PACK>): GBps counts the pack's and that iteration's compulsory bytes over its time, "
                             "ms_pack what the pack adds to it" if fused else "")},

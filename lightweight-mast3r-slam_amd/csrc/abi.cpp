@@ -1056,6 +1056,8 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
   M3S_CHECK(Kp <= M3S_BA_MAX_POSES, "ba: at most 4096 poses (M3S_BA_MAX_POSES)");
   if (cfg->mode == 2) M3S_CHECK(cfg->width > 0 && cfg->height > 0 && (int64_t)cfg->width * cfg->height == N,
                                 "ba calib: height*width must equal the points per keyframe");
+  if (cfg->mode == 2)  // the 12-B calib record holds the matched pixel as u | v << 16 (ba.hip pack_record)
+    M3S_CHECK(cfg->width < 65536 && cfg->height < 65536, "ba calib: width and height must be below 65536");
   if (workspace_bytes < m3s_ba_workspace_size(Kp, N, E)) return fail(M3S_ESPACE, "ba: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   BaPlanImpl P;
@@ -1241,7 +1243,12 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     for (int t = 0; t < EL; t++) RC->slot_of[edge_uid[e0 + t]] = slot[t];
     for (int t = 0; t < EL; t++)
       if (need[t]) pack.push_back(t);
+  } else {
+    for (int t = 0; t < EL; t++) pack.push_back(t);
   }
+  // the pack order: grouped by source keyframe (ba_pack_kernel splits it into eighths, one per XCD, so an XCD's L2
+  // holds the points and confidences of its own source keyframes; the records land in their slots whatever the order)
+  std::stable_sort(pack.begin(), pack.end(), [&](int x, int y) { return ri[e0 + x] < ri[e0 + y]; });
   // the tables the pack and the linearisation read, in ONE upload ahead of the pack; the symbolic tables follow
   // in the same blob (their own upload, at the first solve)
   struct Sec {
@@ -1288,10 +1295,7 @@ int ba_make_plan_impl(const m3s_ba_config* cfg, float* Twc, const float* const* 
     HIP_TRY(hipEventRecord(st.landed, s), "ba stage record");
     st.pending = true;
   }
-  if (!RC) {  // every edge packs into its own slot
-    P.a.rec_slot = nullptr;
-    P.a.pack_list = nullptr;
-  }
+  if (!RC) P.a.rec_slot = nullptr;  // every edge packs into its own slot (the pack list is the source-keyframe order)
   Y->dst = static_cast<char*>(blob) + total;
   HIP_TRY(hipMemsetAsync(P.a.info, 0, 8 * sizeof(int), s), "ba memset");
   HIP_TRY(hipMemsetAsync(P.a.edge_sums, 0, P.edge_sums_bytes > 0 ? P.edge_sums_bytes : 8, s), "ba memset");

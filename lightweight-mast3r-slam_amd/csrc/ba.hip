@@ -129,21 +129,13 @@ __device__ __forceinline__ void actSO3_v(const float* q, const f2* X, f2* Y) {
   Y[2] = X[2] + q[3] * uv2 + (q[0] * uv1 - q[1] * uv0);
 }
 
-// BA_PAIR_ACC: the fp64 accumulators are split between the two lanes of a lane pair (even lane: sums 0..17,
-// odd lane: 18..34), 18 doubles per lane instead of 35, which brings the kernel under the 3-waves-per-SIMD
-// VGPR budget. At each flush a lane hands the partner the run sums the partner owns (DPP swaps) and adds its
-// own and the partner's fp32 run sums of both points in fp64: the same BA_RUN_LEN-point fp32 runs as with
-// per-lane accumulators (folding a lane's two points in fp32 first took the 6-KF rays fixture to 1.6e-5
-// from the fp64 truth, over the 1e-5 contract).
-#ifndef BA_PAIR_ACC
-#define BA_PAIR_ACC 1
-#endif
+// The fp64 accumulation is split between the two lanes of a lane pair (even lane: sums 0..17, odd lane: 18..34). At
+// a flush a lane hands the partner the run sums the partner owns (DPP swaps) and adds its own and the partner's fp32
+// run sums of both points in fp64: the same BA_RUN_LEN-point fp32 runs as with per-lane accumulators (folding a
+// lane's two points in fp32 first took the 6-KF rays fixture to 1.6e-5 from the fp64 truth, over the 1e-5 contract),
+// half the fp64 values to move through LDS.
 #ifndef BA_LIN_WAVES  // waves per SIMD the linearisation is compiled for (VGPR budget 512 / waves)
-#if BA_PAIR_ACC
 #define BA_LIN_WAVES 3
-#else
-#define BA_LIN_WAVES 2
-#endif
 #endif
 #define BA_PAIR_HALF 18  // sums owned per lane of a pair (35 = 18 + 17)
 
@@ -171,7 +163,8 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 }
 
 // Per-call point records (once per gauss_newton call; the GN iterations only move the poses):
-//   rec[e][k] = {Xi (points / rays) or (u_t, v_t, log z_i | NaN if z_i <= z_eps) (calib) ; sw} with
+//   rec[e][k] = {Xi (points / rays) ; sw} (16 B) or, calib, {u_t | v_t << 16, log z_i | NaN if z_i <= z_eps, sw}
+//   (12 B: the lin kernel streams E x N records every iteration, so a quarter less HBM traffic) with
 //   Xi = Xs[i][valid ? idx : 0]
 //   (gn_kernels.cu reads index 0 for an invalid match) and sw = sqrt(q) when the match is valid and
 //   q > Q_thresh, c_i > C_thresh, c_j > C_thresh, else 0 (gn_kernels.cu:880-906) — the per-iteration
@@ -180,25 +173,36 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 // into its record slot.
 // the record of point k of shard edge e (ix, jx: its pose ranks); rays: *n = |Xi| (the record holds Xi / |Xi|,
 // computed with the linearisation's own instruction sequence, so the rows are bit-identical to normalising there)
+#ifndef BA_PACK_NT
+#define BA_PACK_NT 1
+#endif
+#if BA_PACK_NT
+#define BA_NT_LOAD(ptr) __builtin_nontemporal_load(ptr)
+#else
+#define BA_NT_LOAD(ptr) (*(ptr))
+#endif
 template <int MODE>
 __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k,
                                               float* n) {
   const int N = p.N;
   const size_t g = (size_t)(e + p.edge_offset) * N + k;
-  const bool vm = a.valid[g] != 0;
-  const int64_t ind = vm ? a.idx[g] : 0;
+  // the per-edge streams (valid, idx, Q, C_j) are read once: non-temporal, so L2 keeps the source keyframe's X_i /
+  // C_i that the edges of one source (packed back to back on one XCD) gather again
+  const bool vm = BA_NT_LOAD(&a.valid[g]) != 0;
+  const int64_t ind = vm ? BA_NT_LOAD(&a.idx[g]) : 0;
   const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
-  const float q = a.Q[g];
+  const float q = BA_NT_LOAD(&a.Q[g]);
   const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
-                     (a.Ckf[jx][k] * a.Cscale[jx] > p.C_thresh);
+                     (BA_NT_LOAD(&a.Ckf[jx][k]) * a.Cscale[jx] > p.C_thresh);
   // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
   const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
   if constexpr (MODE == BA_MODE_CALIB) {
     const int ind32 = (int)ind;  // < H*W < 2^31: 32-bit division
-    const int v_t = ind32 / p.W, u_t = ind32 - v_t * p.W;
+    const unsigned v_t = (unsigned)(ind32 / p.W), u_t = (unsigned)ind32 - v_t * (unsigned)p.W;  // W, H < 2^16 (plan)
     // log z_i once per call (the same __logf the linearisation applied every iteration), NaN marks z_i <= z_eps
     const float zi = Xi[2];
-    return make_float4((float)u_t, (float)v_t, zi > p.z_eps ? __logf(zi) : __builtin_nanf(""), sw);
+    return make_float4(__builtin_bit_cast(float, u_t | (v_t << 16)), zi > p.z_eps ? __logf(zi) : __builtin_nanf(""),
+                       sw, 0.0f);
   } else if constexpr (MODE == BA_MODE_RAYS) {
     const f2 X[3] = {f2{Xi[0], Xi[0]}, f2{Xi[1], Xi[1]}, f2{Xi[2], Xi[2]}};
     const f2 n2 = X[0] * X[0] + X[1] * X[1] + X[2] * X[2];
@@ -210,22 +214,63 @@ __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p
   }
 }
 
+// a record as stored (pack_record) -> as computed on: calib {u_t, v_t, log z_i, sw} (exact: integers < 2^16)
+template <int MODE>
+__device__ __forceinline__ float4 rec_expand(float4 r) {
+  if constexpr (MODE == BA_MODE_CALIB) {
+    const unsigned uv = __builtin_bit_cast(unsigned, r.x);
+    return make_float4((float)(uv & 0xffffu), (float)(uv >> 16), r.y, r.z);
+  } else {
+    return r;
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void rec_store(float4* slot, int k, float4 r) {
+  // records: streamed out once per call (non-temporal under BA_PACK_NT, like the pack's input streams)
+#if BA_PACK_NT
+  if constexpr (MODE == BA_MODE_CALIB) {
+    typedef float f3v __attribute__((ext_vector_type(3)));
+    __builtin_nontemporal_store(f3v{r.x, r.y, r.z}, reinterpret_cast<f3v*>(reinterpret_cast<float*>(slot) + 3 * (size_t)k));
+  } else {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{r.x, r.y, r.z, r.w}, reinterpret_cast<f4v*>(slot + k));
+  }
+#else
+  if constexpr (MODE == BA_MODE_CALIB) reinterpret_cast<float3*>(slot)[k] = make_float3(r.x, r.y, r.z);
+  else slot[k] = r;
+#endif
+}
+template <int MODE>
+__device__ __forceinline__ float4 rec_load(const float4* slot, int k) {
+  if constexpr (MODE == BA_MODE_CALIB) {
+    const float3 c = reinterpret_cast<const float3*>(slot)[k];
+    return make_float4(c.x, c.y, c.z, 0.0f);
+  } else {
+    return slot[k];
+  }
+}
+
 // record slot s (m3s_ba.h ba_rec_slot_bytes): N records, then the rays' |Xi| at rec + N
 __device__ __forceinline__ float4* rec_of_slot(const BaArgs& a, int s, int N) {
   return reinterpret_cast<float4*>(reinterpret_cast<char*>(a.rec) + (size_t)s * ba_rec_slot_bytes(N));
 }
 
+// XCD partition (gridDim a multiple of 8): the blocks dispatched to XCD x (blockIdx % 8 == x) pack the x-th eighth of
+// the pack list, which the plan orders by source keyframe, so an XCD gathers X_i / C_i of its own source keyframes
+// (measured neutral against one grid-stride over all edges, profiles/r05_ba_pack.txt; kept for the L2 footprint)
 template <int MODE>
 __global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack) {
   const int N = p.N;
-  const size_t total = (size_t)n_pack * N;
-  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
-    const int t = (int)(o / N), k = (int)(o - (size_t)t * N);
+  const int x = blockIdx.x % 8, nloc = gridDim.x / 8;
+  const int t0 = (int)((long long)n_pack * x / 8), t1 = (int)((long long)n_pack * (x + 1) / 8);
+  const size_t total = (size_t)(t1 - t0) * N;
+  for (size_t o = (size_t)(blockIdx.x / 8) * blockDim.x + threadIdx.x; o < total; o += (size_t)nloc * blockDim.x) {
+    const int t = t0 + (int)(o / N), k = (int)(o % N);
     const int e = a.pack_list ? a.pack_list[t] : t;
     float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
     float n = 0.0f;
-    rec[k] = pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n);
-    if constexpr (MODE == BA_MODE_RAYS) reinterpret_cast<float*>(rec + N)[k] = n;
+    rec_store<MODE>(rec, k, pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n));
+    if constexpr (MODE == BA_MODE_RAYS) __builtin_nontemporal_store(n, reinterpret_cast<float*>(rec + N) + k);
   }
 }
 
@@ -314,18 +359,13 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       Tij[c] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, Tij[c])));
   }
 #endif
-#if BA_PAIR_ACC
-  const bool odd = threadIdx.x & 1;
-  double acc[BA_PAIR_HALF];
-#pragma unroll
-  for (int m = 0; m < BA_PAIR_HALF; m++) acc[m] = 0.0;
-#else
-  double L[28], v[7];
-#pragma unroll
-  for (int c = 0; c < 28; c++) L[c] = 0.0;
-#pragma unroll
-  for (int c = 0; c < 7; c++) v[c] = 0.0;
-#endif
+  // the block's fp64 sums: a flush transposes the lanes' fp64 pair sums through LDS (s_fl: conflict-free, one
+  // column per thread) and 7 threads per sum add its 128 lanes, then the 7 partials in order: ~40 instructions per
+  // thread instead of a 6-level fp64 shuffle butterfly per sum (~110 VALU per sum and wave, ~15 % of the kernel)
+  __shared__ double s_fl[BA_PAIR_HALF][256];
+  __shared__ double s_red[35][7];
+  __shared__ double s_tot[BA_NSUM];
+  if (threadIdx.x < BA_NSUM) s_tot[threadIdx.x] = 0.0;
   float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
   float* rec_n = reinterpret_cast<float*>(rec + N);  // rays: |Xi|
   const float* Xj_base = a.Xkf[jx];
@@ -337,42 +377,46 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
   for (int c = 0; c < 28; c++) fL[c] = f2{0.0f, 0.0f};
 #pragma unroll
   for (int c = 0; c < 7; c++) fv[c] = f2{0.0f, 0.0f};
-  int run = 0;
-  // two points per lane per round, (k0, k0 + blockDim): every per-point float operation runs on both at once
-  // as one packed fp32 instruction (v_pk_fma/mul/add_f32; float2 lanes), the transcendentals per component
-  // a block-uniform trip count: every lane reaches each run flush together (the pair flush swaps run sums
-  // between the lanes of a pair); a lane past the chunk's end skips the point work
-  for (int k00 = k_begin; k00 < k_end; k00 += 2 * blockDim.x) {
-    const int k0 = k00 + (int)threadIdx.x;
-    if (k0 < k_end) {
-    const int k1 = k0 + (int)blockDim.x;
-    const bool has1 = k1 < k_end;
-    // a missing second point repeats the first with weight 0: it adds exact zeros unless the first point's own
-    // row is non-finite, which poisons the sums anyway (another point as filler changed the rays sums)
-    const int k1c = has1 ? k1 : k0;
-    float4 R0, R1;
-    f2 nI = {0.0f, 0.0f};  // rays: |Xi| of both points
-    if constexpr (PACK) {
-      float n0 = 0.0f, n1 = 0.0f;
-      R0 = pack_record<MODE>(a, p, e, ix, jx, k0, &n0);
-      n1 = n0;
-      if (has1) R1 = pack_record<MODE>(a, p, e, ix, jx, k1, &n1);
-      else R1 = R0;
-      nI = f2{n0, n1};
-      rec[k0] = R0;
-      if (has1) rec[k1] = R1;
-      if constexpr (MODE == BA_MODE_RAYS) {
-        rec_n[k0] = nI.x;
-        if (has1) rec_n[k1] = nI.y;
-      }
-    } else {
-      R0 = rec[k0];
-      R1 = rec[k1c];
-      if constexpr (MODE == BA_MODE_RAYS) nI = f2{rec_n[k0], rec_n[k1c]};
-    }
-    f2 Xj[3];
+  // a run's fp32 sums into the block's fp64 sums: the lanes of a pair trade the halves they own (pair_flush: fp64
+  // adds from 0 in the order a per-lane accumulator would make them), then the LDS transpose above. A chunk is at
+  // most BA_RUN_LEN rounds (ba_chunks), so this runs once per block and no fp64 accumulator is live across the point
+  // loop: its VGPRs carry the next round's prefetched records instead. Block-uniform (barriers): every thread of
+  // the block reaches every flush (the trip count is the block's).
+  auto flush = [&]() {
+    const int t = threadIdx.x;
+    const bool odd = t & 1;
+    double acc[BA_PAIR_HALF];
 #pragma unroll
-    for (int c = 0; c < 3; c++) Xj[c] = f2{Xj_base[(size_t)k0 * 3 + c], Xj_base[(size_t)k1c * 3 + c]};
+    for (int m = 0; m < BA_PAIR_HALF; m++) acc[m] = 0.0;
+    pair_flush(acc, fL, fv, odd);
+#pragma unroll
+    for (int m = 0; m < BA_PAIR_HALF; m++) s_fl[m][t] = acc[m];
+    __syncthreads();
+    if (t < 35 * 7) {  // sum c: even lanes own 0..17, odd lanes 18..34
+      const int c = t / 7, part = t - 7 * c;
+      const int par = c >= BA_PAIR_HALF ? 1 : 0, m = c - BA_PAIR_HALF * par;
+      double r = 0.0;
+      for (int i = part; i < 128; i += 7) r += s_fl[m][2 * i + par];
+      s_red[c][part] = r;
+    }
+    __syncthreads();
+    if (t < 35) {
+      double r = s_tot[t];
+#pragma unroll
+      for (int q = 0; q < 7; q++) r += s_red[t][q];
+      s_tot[t] = r;
+    }
+#pragma unroll
+    for (int c = 0; c < 28; c++) fL[c] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 7; c++) fv[c] = f2{0.0f, 0.0f};
+  };
+  // the rows of one round: two points per lane, (k0, k0 + blockDim): every per-point float operation runs on both at
+  // once as one packed fp32 instruction (v_pk_fma/mul/add_f32; float2 lanes), the transcendentals per component.
+  // R0, R1: the records as computed on (rec_expand); a missing second point (has1 false) repeats the first with
+  // weight 0: it adds exact zeros unless the first point's own row is non-finite, which poisons the sums anyway
+  // (another point as filler changed the rays sums)
+  auto rows = [&](const float4& R0, const float4& R1, f2 nI, const f2* Xj, bool has1) {
     const f2 Rx = {R0.x, R1.x}, Ry = {R0.y, R1.y}, Rz = {R0.z, R1.z};
     // sqrt(q), 0 for an invalid match (ba_pack) and for the missing second point of a ragged tail
     const f2 sqq = {R0.w, has1 ? R1.w : 0.0f};
@@ -454,72 +498,77 @@ __global__ void __launch_bounds__(256, BA_LIN_WAVES) ba_lin_kernel(BaArgs a, BaP
       acc_local_f2<0b0111110>(fL, fv, J1, huber_ba2(swp * err[1]) * wp, err[1]);  // {1,2,3,4,5}
       acc_local_f2<0b1011100>(fL, fv, J2, huber_ba2(swd * err[2]) * wd, err[2]);  // {2,3,4,6}
     }
-    }
-    if (++run == BA_RUN_LEN) {  // the run's fp32 sums (BA_RUN_LEN points per slot) into the fp64 accumulators
-      run = 0;
-#if BA_PAIR_ACC
-      pair_flush(acc, fL, fv, odd);
+  };
+  int run = 0;
+  // a block-uniform trip count: every lane reaches each run flush together (the pair flush swaps run sums between
+  // the lanes of a pair); a lane past the chunk's end skips the point work
+  if constexpr (PACK) {
+    for (int k00 = k_begin; k00 < k_end; k00 += 2 * blockDim.x) {
+      const int k0 = k00 + (int)threadIdx.x;
+      if (k0 < k_end) {
+        const int k1 = k0 + (int)blockDim.x;
+        const bool has1 = k1 < k_end;
+        const int k1c = has1 ? k1 : k0;
+        float n0 = 0.0f, n1 = 0.0f;
+        float4 R0 = pack_record<MODE>(a, p, e, ix, jx, k0, &n0), R1;
+        n1 = n0;
+        if (has1) R1 = pack_record<MODE>(a, p, e, ix, jx, k1, &n1);
+        else R1 = R0;
+        rec_store<MODE>(rec, k0, R0);
+        if (has1) rec_store<MODE>(rec, k1, R1);
+        if constexpr (MODE == BA_MODE_RAYS) {
+          rec_n[k0] = n0;
+          if (has1) rec_n[k1] = n1;
+        }
+        f2 Xj[3];
 #pragma unroll
-      for (int c = 0; c < 28; c++) fL[c] = f2{0.0f, 0.0f};
-#pragma unroll
-      for (int c = 0; c < 7; c++) fv[c] = f2{0.0f, 0.0f};
-#else
-#pragma unroll
-      for (int c = 0; c < 28; c++) {
-        L[c] += (double)fL[c].x;
-        L[c] += (double)fL[c].y;
-        fL[c] = f2{0.0f, 0.0f};
+        for (int c = 0; c < 3; c++) Xj[c] = f2{Xj_base[(size_t)k0 * 3 + c], Xj_base[(size_t)k1c * 3 + c]};
+        rows(rec_expand<MODE>(R0), rec_expand<MODE>(R1), f2{n0, n1}, Xj, has1);
       }
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        v[c] += (double)fv[c].x;
-        v[c] += (double)fv[c].y;
-        fv[c] = f2{0.0f, 0.0f};
+      if (++run == BA_RUN_LEN) {
+        run = 0;
+        flush();
       }
-#endif
+    }
+  } else {
+    // software-pipelined: a lane loads the next round's records and X_j before it computes this round's rows, so
+    // the loads' HBM latency runs under the VALU work (the kernel holds 3 waves per SIMD, too few to hide it alone).
+    // Every load is unconditional (a lane past the chunk's end loads point k_begin and skips the rows): the hand-over
+    // nxt -> cur at the end of a round is then the only use of a load in flight, after the round's rows.
+    struct Round {
+      float4 R0, R1;  // as stored (rec_load)
+      f2 nI;          // rays: |Xi| of both points
+      f2 Xj[3];
+    };
+    auto fetch = [&](int k00, Round& r) {
+      const int k0 = k00 + (int)threadIdx.x < k_end ? k00 + (int)threadIdx.x : k_begin;
+      const int k1 = k0 + (int)blockDim.x < k_end ? k0 + (int)blockDim.x : k0;
+      r.R0 = rec_load<MODE>(rec, k0);
+      r.R1 = rec_load<MODE>(rec, k1);
+      if constexpr (MODE == BA_MODE_RAYS) r.nI = f2{rec_n[k0], rec_n[k1]};
+#pragma unroll
+      for (int c = 0; c < 3; c++) r.Xj[c] = f2{Xj_base[(size_t)k0 * 3 + c], Xj_base[(size_t)k1 * 3 + c]};
+    };
+    Round cur;
+    fetch(k_begin, cur);
+    for (int k00 = k_begin; k00 < k_end; k00 += 2 * blockDim.x) {
+      const int k0 = k00 + (int)threadIdx.x;
+      Round nxt;
+      fetch(k00 + 2 * blockDim.x, nxt);
+      if (k0 < k_end) {
+        f2 nI = {0.0f, 0.0f};
+        if constexpr (MODE == BA_MODE_RAYS) nI = cur.nI;
+        rows(rec_expand<MODE>(cur.R0), rec_expand<MODE>(cur.R1), nI, cur.Xj, k0 + (int)blockDim.x < k_end);
+      }
+      if (++run == BA_RUN_LEN) {
+        run = 0;
+        flush();
+      }
+      cur = nxt;
     }
   }
-  __shared__ double s_part[4][BA_NSUM];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#if BA_PAIR_ACC
-  pair_flush(acc, fL, fv, odd);
-  // butterfly over the lanes of one parity (offsets 32..2), then 4 waves through LDS
-#pragma unroll
-  for (int m = 0; m < BA_PAIR_HALF; m++) {
-    double t = acc[m];
-#pragma unroll
-    for (int off = 32; off > 1; off >>= 1) t += __shfl_xor(t, off, 64);
-    const int c = odd ? BA_PAIR_HALF + m : m;
-    if (lane < 2 && c < 35) s_part[wid][c] = t;
-  }
-#else
-#pragma unroll
-  for (int c = 0; c < 28; c++) {
-    L[c] += (double)fL[c].x;
-    L[c] += (double)fL[c].y;
-  }
-#pragma unroll
-  for (int c = 0; c < 7; c++) {
-    v[c] += (double)fv[c].x;
-    v[c] += (double)fv[c].y;
-  }
-  // wave64 butterfly in fp64, then 4 waves through LDS
-#pragma unroll
-  for (int c = 0; c < 28; c++) {
-    const double t = wave_sum(L[c]);
-    if (lane == 0) s_part[wid][c] = t;
-  }
-#pragma unroll
-  for (int c = 0; c < 7; c++) {
-    const double t = wave_sum(v[c]);
-    if (lane == 0) s_part[wid][28 + c] = t;
-  }
-#endif
-  __syncthreads();
-  if (threadIdx.x < 35) {
-    const int c = threadIdx.x;
-    a.partials[(size_t)code * BA_NSUM + c] = s_part[0][c] + s_part[1][c] + s_part[2][c] + s_part[3][c];
-  }
+  flush();
+  if (threadIdx.x < 35) a.partials[(size_t)code * BA_NSUM + threadIdx.x] = s_tot[threadIdx.x];  // its own entry
 }
 
 // per-edge: sum chunk partials, M = A L A^T, g = A v with A the adjoint-inverse map of T_i.
@@ -1532,7 +1581,7 @@ extern "C" hipError_t m3s_launch_ba_kf_compare(const BaKfCopy* kf, int Kp, int N
 extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int n_pack, hipStream_t s) {
   if (n_pack <= 0) return hipSuccess;
   const size_t total = (size_t)n_pack * p->N;
-  const dim3 g((unsigned)std::min<size_t>((total + 255) / 256, 8192));
+  const dim3 g((unsigned)std::max<size_t>(8, std::min<size_t>((total + 255) / 256, 8192) & ~(size_t)7));  // x8: XCDs
   if (p->mode == BA_MODE_CALIB)
     hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, n_pack);
   else if (p->mode == BA_MODE_RAYS)

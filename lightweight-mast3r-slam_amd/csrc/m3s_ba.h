@@ -38,7 +38,7 @@ struct BaKfCopy {
   float* copy;
 };
 
-// bytes of one record slot: N 16-B records, then N floats (rays: |Xi|) padded to 16 B. A slot's bytes sit at
+// bytes of one record slot: N 16-B records (calib uses 12 B of each), then N floats (rays: |Xi|) padded to 16 B. A slot's bytes sit at
 // slot * ba_rec_slot_bytes(N) whatever the plan's edge count: record reuse keeps slots across the plans of a growing
 // graph, and a region [all records | all |Xi|] would move its second part with the edge count
 __host__ __device__ inline size_t ba_rec_slot_bytes(int N) { return (size_t)16 * N + (size_t)4 * ((N + 3) & ~3); }
@@ -53,10 +53,10 @@ struct BaArgs {
   const int64_t* idx;    // (E,N) global edge rows
   const uint8_t* valid;  // (E,N)
   const float* Q;        // (E,N)
-  float4* rec;           // record slots (ba_rec_slot_bytes each): N point records {Xi | Xi/|Xi| (rays) | u_t, v_t,
-                         // log z_i ; sqrt-weight}, then (rays) N floats |Xi|
+  float4* rec;           // record slots (ba_rec_slot_bytes each): N point records {Xi | Xi/|Xi| (rays) ; sqrt-weight}
+                         // (16 B) or {u_t | v_t << 16, log z_i, sqrt-weight} (calib, 12 B), then (rays) N floats |Xi|
   const int* rec_slot;   // (E_local) record slot of each shard edge (record reuse across plans), or null: slot = edge
-  const int* pack_list;  // (n_pack) shard edges the pack writes (the others kept their records), or null: all
+  const int* pack_list;  // (n_pack) shard edges the pack writes, grouped by source keyframe (reuse: only the changed)
   double* partials;      // (E_local*chunks, 36)
   double* edge_sums;     // (E, 36) global edge rows; all-reduced across ranks in multi-GPU BA
   // block-sparse pose system (ba_pattern.h; analysed once per plan, factored on the device every iteration)

@@ -313,3 +313,26 @@ def test_workspace_release_entry_points_are_safe_without_state():
         fn.restype = ctypes.c_int
         assert fn(ctypes.c_void_p(0x1234000)) == 0
         assert fn(None) == 0
+
+
+def test_isa_spill_check_flags_spilling_kernels(tmp_path):
+    """scripts/isa_check_spills.py (the Makefile's no-spill gate on refine_tile_kernel and ba_lin_kernel) fails on a
+    named kernel whose AMDGPU metadata reports spilled VGPRs, passes when none do, and fails when no kernel matches."""
+    import subprocess
+    import sys
+
+    def meta(name, spills):
+        return (f"  - .agpr_count:     0\n    .args:\n      - .offset:         0\n        .size:           8\n"
+                f"    .name:           {name}\n    .sgpr_spill_count: 0\n    .vgpr_count:     128\n"
+                f"    .vgpr_spill_count: {spills}\n    .wavefront_size: 64\n")
+
+    script = os.path.join(os.path.dirname(__file__), "..", "scripts", "isa_check_spills.py")
+    run = lambda text, *names: subprocess.run([sys.executable, script, str(tmp_path / "k.s"), *names],
+                                              capture_output=True, text=True) if (tmp_path / "k.s").write_text(text) \
+        else None
+    ok = run("amdhsa.kernels:\n" + meta("_Z10refine_tile_kernelILi1EEvv", 0) + meta("_Z5otherv", 9), "refine_tile")
+    assert ok.returncode == 0, ok.stdout
+    bad = run("amdhsa.kernels:\n" + meta("_Z10refine_tile_kernelILi1EEvv", 3), "refine_tile")
+    assert bad.returncode == 1 and "3 spilled VGPRs" in bad.stdout
+    none = run("amdhsa.kernels:\n" + meta("_Z5otherv", 0), "refine_tile")
+    assert none.returncode == 1
