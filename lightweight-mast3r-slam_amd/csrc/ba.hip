@@ -181,19 +181,10 @@ __device__ __forceinline__ void pair_flush(double* acc, const f2* fL, const f2* 
 #else
 #define BA_NT_LOAD(ptr) (*(ptr))
 #endif
+// the record of a matched point from its gathered X_i (ind: its pixel in keyframe i) and its folded validity
 template <int MODE>
-__device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k,
+__device__ __forceinline__ float4 pack_finish(const BaParams& p, const float* Xi, int64_t ind, float q, bool valid,
                                               float* n) {
-  const int N = p.N;
-  const size_t g = (size_t)(e + p.edge_offset) * N + k;
-  // the per-edge streams (valid, idx, Q, C_j) are read once: non-temporal, so L2 keeps the source keyframe's X_i /
-  // C_i that the edges of one source (packed back to back on one XCD) gather again
-  const bool vm = BA_NT_LOAD(&a.valid[g]) != 0;
-  const int64_t ind = vm ? BA_NT_LOAD(&a.idx[g]) : 0;
-  const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
-  const float q = BA_NT_LOAD(&a.Q[g]);
-  const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
-                     (BA_NT_LOAD(&a.Ckf[jx][k]) * a.Cscale[jx] > p.C_thresh);
   // hardware sqrt (<= 1 ulp): parity is checked against the fp64 truth (1e-5)
   const float sw = valid ? __builtin_amdgcn_sqrtf(q) : 0.0f;
   if constexpr (MODE == BA_MODE_CALIB) {
@@ -212,6 +203,21 @@ __device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p
   } else {
     return make_float4(Xi[0], Xi[1], Xi[2], sw);
   }
+}
+
+// the record of point k of shard edge e (ix, jx: its pose ranks), every load in order (the fused pack of the first
+// linearisation, ba_lin_kernel<PACK>); the per-edge streams are non-temporal
+template <int MODE>
+__device__ __forceinline__ float4 pack_record(const BaArgs& a, const BaParams& p, int e, int ix, int jx, int k,
+                                              float* n) {
+  const size_t g = (size_t)(e + p.edge_offset) * p.N + k;
+  const bool vm = BA_NT_LOAD(&a.valid[g]) != 0;
+  const int64_t ind = vm ? BA_NT_LOAD(&a.idx[g]) : 0;
+  const float* Xi = a.Xkf[ix] + (size_t)ind * 3;
+  const float q = BA_NT_LOAD(&a.Q[g]);
+  const bool valid = vm && (q > p.Q_thresh) && (a.Ckf[ix][ind] * a.Cscale[ix] > p.C_thresh) &&
+                     (BA_NT_LOAD(&a.Ckf[jx][k]) * a.Cscale[jx] > p.C_thresh);
+  return pack_finish<MODE>(p, Xi, ind, q, valid, n);
 }
 
 // a record as stored (pack_record) -> as computed on: calib {u_t, v_t, log z_i, sw} (exact: integers < 2^16)
@@ -255,22 +261,66 @@ __device__ __forceinline__ float4* rec_of_slot(const BaArgs& a, int s, int N) {
   return reinterpret_cast<float4*>(reinterpret_cast<char*>(a.rec) + (size_t)s * ba_rec_slot_bytes(N));
 }
 
-// XCD partition (gridDim a multiple of 8): the blocks dispatched to XCD x (blockIdx % 8 == x) pack the x-th eighth of
-// the pack list, which the plan orders by source keyframe, so an XCD gathers X_i / C_i of its own source keyframes
-// (measured neutral against one grid-stride over all edges, profiles/r05_ba_pack.txt; kept for the L2 footprint)
+// One block per tile of BA_PACK_TILE points of one edge: the edge's slot, ranks, keyframe pointers and confidence
+// scales are block-uniform (scalar loads, once per block, not per point). A lane takes BA_PACK_UNROLL points per trip
+// (256 apart): every per-point stream load (valid, idx, Q, C_j; non-temporal, unconditional at a clamped index) is
+// issued first, then the X_i / C_i gathers, then the stores, so a point's chain is two loads deep and the trip's
+// points overlap. Tiles in XCD-contiguous order: the blocks of XCD x (blockIdx % 8 == x) take the x-th eighth of
+// the tile list, whose edges the plan orders by source keyframe, so an XCD gathers its own source keyframes' X_i / C_i.
+#ifndef BA_PACK_TILE
+#define BA_PACK_TILE 4096
+#endif
+#ifndef BA_PACK_UNROLL
+#define BA_PACK_UNROLL 4
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack) {
+__global__ void __launch_bounds__(256) ba_pack_kernel(BaArgs a, BaParams p, int n_pack, int tiles_per_edge) {
+  constexpr int U = BA_PACK_UNROLL;
   const int N = p.N;
-  const int x = blockIdx.x % 8, nloc = gridDim.x / 8;
-  const int t0 = (int)((long long)n_pack * x / 8), t1 = (int)((long long)n_pack * (x + 1) / 8);
-  const size_t total = (size_t)(t1 - t0) * N;
-  for (size_t o = (size_t)(blockIdx.x / 8) * blockDim.x + threadIdx.x; o < total; o += (size_t)nloc * blockDim.x) {
-    const int t = t0 + (int)(o / N), k = (int)(o % N);
-    const int e = a.pack_list ? a.pack_list[t] : t;
-    float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
-    float n = 0.0f;
-    rec_store<MODE>(rec, k, pack_record<MODE>(a, p, e, a.ii_rank[e], a.jj_rank[e], k, &n));
-    if constexpr (MODE == BA_MODE_RAYS) __builtin_nontemporal_store(n, reinterpret_cast<float*>(rec + N) + k);
+  const int n_tiles = n_pack * tiles_per_edge;
+  const int tile = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;  // gridDim.x: a multiple of 8
+  if (tile >= n_tiles) return;
+  const int t = tile / tiles_per_edge, c = tile - t * tiles_per_edge;
+  const int e = a.pack_list ? a.pack_list[t] : t;
+  const int ix = a.ii_rank[e], jx = a.jj_rank[e];
+  const float* __restrict__ Xi = a.Xkf[ix];
+  const float* __restrict__ Ci = a.Ckf[ix];
+  const float* __restrict__ Cj = a.Ckf[jx];
+  const float si = a.Cscale[ix], sj = a.Cscale[jx];
+  float4* rec = rec_of_slot(a, a.rec_slot ? a.rec_slot[e] : e, N);
+  const size_t g0 = (size_t)(e + p.edge_offset) * N;
+  const int k_begin = c * BA_PACK_TILE, k_end = min(N, k_begin + BA_PACK_TILE);
+  for (int k0 = k_begin + (int)threadIdx.x; k0 < k_end; k0 += 256 * U) {
+    unsigned char vm[U];
+    int64_t id[U];
+    float q[U], cj[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = min(k0 + 256 * u, k_end - 1);
+      vm[u] = BA_NT_LOAD(&a.valid[g0 + k]);
+      id[u] = BA_NT_LOAD(&a.idx[g0 + k]);
+      q[u] = BA_NT_LOAD(&a.Q[g0 + k]);
+      cj[u] = BA_NT_LOAD(&Cj[k]);
+    }
+    float X[U][3], ci[U];
+    int64_t ind[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      ind[u] = vm[u] ? id[u] : 0;  // gn_kernels.cu reads index 0 for an invalid match
+      X[u][0] = Xi[(size_t)ind[u] * 3];
+      X[u][1] = Xi[(size_t)ind[u] * 3 + 1];
+      X[u][2] = Xi[(size_t)ind[u] * 3 + 2];
+      ci[u] = Ci[ind[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = k0 + 256 * u;
+      if (k >= k_end) continue;
+      const bool valid = vm[u] && (q[u] > p.Q_thresh) && (ci[u] * si > p.C_thresh) && (cj[u] * sj > p.C_thresh);
+      float n = 0.0f;
+      rec_store<MODE>(rec, k, pack_finish<MODE>(p, X[u], ind[u], q[u], valid, &n));
+      if constexpr (MODE == BA_MODE_RAYS) __builtin_nontemporal_store(n, reinterpret_cast<float*>(rec + N) + k);
+    }
   }
 }
 
@@ -1580,14 +1630,16 @@ extern "C" hipError_t m3s_launch_ba_kf_compare(const BaKfCopy* kf, int Kp, int N
 
 extern "C" hipError_t m3s_launch_ba_pack(const BaArgs* a, const BaParams* p, int n_pack, hipStream_t s) {
   if (n_pack <= 0) return hipSuccess;
-  const size_t total = (size_t)n_pack * p->N;
-  const dim3 g((unsigned)std::max<size_t>(8, std::min<size_t>((total + 255) / 256, 8192) & ~(size_t)7));  // x8: XCDs
+  const int tiles = (p->N + BA_PACK_TILE - 1) / BA_PACK_TILE;
+  const size_t blocks = ((size_t)n_pack * tiles + 7) & ~(size_t)7;  // a multiple of 8: the XCD-contiguous tile order
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  const dim3 g((unsigned)blocks);
   if (p->mode == BA_MODE_CALIB)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, n_pack);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_CALIB>, g, dim3(256), 0, s, *a, *p, n_pack, tiles);
   else if (p->mode == BA_MODE_RAYS)
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, n_pack);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_RAYS>, g, dim3(256), 0, s, *a, *p, n_pack, tiles);
   else
-    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, n_pack);
+    hipLaunchKernelGGL(m3s::ba_pack_kernel<BA_MODE_POINTS>, g, dim3(256), 0, s, *a, *p, n_pack, tiles);
   return hipGetLastError();
 }
 
