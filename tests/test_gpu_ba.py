@@ -403,6 +403,35 @@ def test_pack_fused_into_first_linearisation_is_bit_identical(mode, monkeypatch)
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize("mode", ["points", "rays", "calib"])
+def test_pack_tiles_with_ragged_last_tile(mode, monkeypatch):
+    """The pack kernel's tiles (ba.hip ba_pack_kernel: one block per 4096 points of one edge, 4 points per lane per
+    trip, loads at a clamped index) on 72x100 = 7200 points per edge: one full tile and a ragged one whose last
+    trip is partly past the edge. Its records must equal the fused pack's (ba_lin_kernel<PACK>: pack_record, one
+    point at a time, every load in order) bit for bit, and the poses sit within 1e-5 of the fp64 truth."""
+    from m3s.synthetic import make_graph, two_way
+
+    H, W = 72, 100
+    G = make_graph(n_kf=8, H=H, W=W, seed=13)
+    ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
+    K = G["K"].numpy()
+    Xs = G["Xs"].numpy()
+    if mode == "calib":
+        Xs = O.backproject_constrain(Xs, K, (H, W))
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("M3S_BA_FUSED_PACK", fused)
+        out.append(_call(mode, G["Twc0"].numpy(), Xs, G["Cs"].numpy(), ii, jj, idx, valid, Q, K, H, W))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    sa, sb = SIG[mode]
+    p = O.ba_params(mode, sa, sb, 0.0, 1.5, K=K, height=H, width=W, pixel_border=-10, z_eps=1e-6)
+    Cs = G["Cs"].numpy()
+    T_ref, _, _ = O.gauss_newton_f64(mode, G["Twc0"].numpy().astype(np.float64), Xs.astype(np.float64),
+                                     Cs[..., 0].astype(np.float64), ii, jj, idx, valid[..., 0],
+                                     Q[..., 0].astype(np.float64), p, 10, 1e-8)
+    np.testing.assert_allclose(out[1][0], T_ref, atol=1e-5)
+
+
 @pytest.mark.timeout(300)
 def test_sharded_hip_path_world2(tmp_path):
     """the product's sharded BA (HipShard over libm3s.so + run_sharded) at N = 2. Two fresh
