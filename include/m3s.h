@@ -154,7 +154,7 @@ int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /*
  * fallback factorisation is used, [5] = distinct target keyframes among the shard's edges, [6] = shard edges,
  * [7] = poses, [8] = factor steps run by the optional frontal or subtree phase (one
  * launch), [9] = its workgroups, [10] = supernodes of the supernodal factorisation (0: the column-task one),
- * [11] = its multi-workgroup launch's workgroups. info holds 12 ints. */
+ * [11] = its multi-workgroup launch's workgroups, [12] = poses of the dense top phase (0: none). info holds 13 ints. */
 int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info);
 /* Host-only diagnostic of the symbolic factorisation the plan builds for these edges (host arrays):
  * stats[0] = factor blocks (7x7, diagonal included), [1] = elimination-tree levels, [2] = update groups

@@ -557,7 +557,8 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_SYM_SECTIONS = 20;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_SYM_SECTIONS = 21;  // the symbolic half's sections (build_symbolic)
+constexpr int BA_TOP_MAX = 25;  // ba.hip TOP_MAX: poses of the dense top phase at most (its LDS: 7T x 7T packed + panels)
 constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
 constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
 constexpr int BA_SP_PLAN_BYTES = 144 * 1024;  // ba.hip SP_PLAN_BYTES: LDS of the one-workgroup factor kernel
@@ -591,7 +592,8 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       (size_t)nb * (4 + 16 + 2 * (BA_MAX_WIDE_STEPS + 1) + 4) + 8 * (nb + 2 * nLm) + 4 * nLm +
                       ba_max_pairs(Kp) + nLm + nb + 8 * (size_t)nb + nLm +
                       2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm) +  // + the dataflow schedule
-                      ba_sn_capacity(Kp);                                    // + the supernodal plan
+                      ba_sn_capacity(Kp) +                                   // + the supernodal plan
+                      4 + BA_TOP_MAX + BA_TOP_MAX * BA_TOP_MAX;              // + the dense top phase
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -736,6 +738,7 @@ struct PlanSym {
   int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
   int front_cut = 0, front_wgs = 0, front_napply = 0;  // frontal subtree phase (ba_front_kernel), see build_symbolic
   int snode = 0, sn_wgs = 0, nsn = 0;  // supernodal factorisation (ba_snode_kernel): its bottom workgroups, supernodes
+  int top_T = 0, top_lev = 0;          // dense top phase (ba_dense_top_kernel): its poses, its first elimination level
   bool pack_deferred = false;    // the plan's pack runs inside its first linearisation (set at plan time, under g_sym_mu)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
@@ -921,9 +924,27 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
       Y->step_tasks[l] = (int)step_rec.size() / 8 - Y->step_base[l];
     }
   }
+  // Dense top phase (M3S_BA_TOP=t, an option): the root end of the elimination tree, the lowest level cut whose
+  // columns number at most t (<= BA_TOP_MAX) poses, factored densely on the matrix cores (ba_dense_top_kernel) between a
+  // factor-only and a back-substitution-only run of the one-workgroup kernel
+  std::vector<int> toptab;
+  {
+    const char* tenv = getenv("M3S_BA_TOP");
+    const int tmax = tenv && *tenv ? std::min(atoi(tenv), BA_TOP_MAX) : 0;
+    if (tmax >= 2 && flow_on && !Y->dense && !Y->snode && Y->sub_cut == 0 && Y->front_cut == 0)
+      for (int l = std::max(Y->wide_steps, 1); l < S.nlev; l++)
+        if (S.nb - S.lev_ptr[l] <= tmax) {
+          if (S.nb - S.lev_ptr[l] >= 2 && ba_top_plan(S, l, &toptab) > 0) {
+            Y->top_T = toptab[0];
+            Y->top_lev = l;
+          }
+          break;
+        }
+  }
   // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
   // (supernodal: a schedule of the back substitution alone, every column factored before the kernel starts)
-  if (flow_on || Y->snode) ba_flow_schedule(S, Y->snode ? S.nlev + 1 : Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut);
+  if (flow_on || Y->snode)
+    ba_flow_schedule(S, Y->snode ? S.nlev + 1 : Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut, Y->top_lev);
   Y->flow = sched.empty() ? 0 : 1;
   if (Y->flow && !flow_fits(sched)) {  // the kernel would run level-synchronously: drop the schedule (and say so)
     Y->flow = 0;
@@ -937,10 +958,20 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     Y->err = "ba: the subtree phase needs the dataflow schedule";
     return M3S_EINVAL;
   }
+  if (!Y->flow && Y->top_T > 0) {  // a schedule without the top columns that does not fit: no top phase
+    Y->top_T = Y->top_lev = 0;
+    toptab.clear();
+    if (flow_on) {
+      ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut, 0);
+      Y->flow = flow_fits(sched) ? 1 : 0;
+      if (!Y->flow) sched.clear();
+    }
+  }
   const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
                                                    &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
                                                    &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
-                                                   &step_rec, &subtab,  &fronttab,  &frontapply, &sntab};
+                                                   &step_rec, &subtab,  &fronttab,  &frontapply, &sntab,
+                                                   &toptab};
   size_t total = 0;
   for (int k = 0; k < BA_SYM_SECTIONS; k++) {
     Y->off[k] = total;
@@ -1022,7 +1053,8 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
       (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
       (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
       (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec,
-      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply, (const void**)&a.sn_tab};
+      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply, (const void**)&a.sn_tab,
+      (const void**)&a.top_tab};
   for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
@@ -1038,6 +1070,7 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   a.front_u = a.L + (size_t)Y->nL * 64;
   a.snode = Y->snode;
   a.sn_wgs = Y->sn_wgs;
+  a.top_T = Y->top_T;
   return a;
 }
 
@@ -1470,6 +1503,7 @@ extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   info[9] = Y->front_wgs > 0 ? Y->front_wgs : Y->sub_wgs;
   info[10] = Y->snode ? Y->nsn : 0;
   info[11] = Y->snode ? Y->sn_wgs : 0;
+  info[12] = Y->top_T;
   return M3S_OK;
 }
 

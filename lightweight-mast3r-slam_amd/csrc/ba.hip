@@ -1467,8 +1467,182 @@ __global__ void __launch_bounds__(64) ba_front_apply_kernel(BaArgs a) {
   }
 }
 
+// ---- dense top phase (ba_pattern.h ba_top_plan; M3S_BA_TOP) ----
+// The root end of the elimination tree (T <= TOP_MAX poses at levels >= the plan's cut) holds a nearly dense factor:
+// instead of one dependent column task per level, ONE workgroup factors its n = 7T rows densely, after the factor-only
+// run of the one-workgroup kernel applied every update from the columns below. Right-looking over 7-column panels
+// (one pose each):
+//   (a) the owners of the panel's columns write them (rows >= c0) from their accumulator tiles to LDS;
+//   (b) wave 0 factors the 7x7 diagonal block in registers (rows in lanes 0-6, the rhs in lane 7: forward
+//       substitution y_p = L_pp^-1 b_p), the same pivot arithmetic as sp_factor_column_at;
+//   (c) one thread per row below solves x L_pp^T = a (the panel of L) and updates its rhs entry;
+//   (d) every wave updates its trailing 16x16 tiles, C -= P P^T, on the matrix cores (v_mfma_f64_16x16x4, K = 7
+//       padded to 8; the tiles stay in registers across panels).
+// Then the back substitution from the root down (x_p = L_pp^-T z_p, z of the poses before it updated right-looking)
+// and x into a.xs (factor order) for the back-substitution-only run. Deterministic (fixed ownership and order); not
+// bit-identical to the column-task factor (other summation order).
+typedef double d4v __attribute__((ext_vector_type(4)));
+constexpr int TOP_MAX = 25;
+constexpr int TOP_NMAX = 7 * TOP_MAX;                  // 175 rows at most
+constexpr int TOP_NP = ((TOP_NMAX + 15) / 16) * 16;   // 176: whole 16-row tiles
+constexpr int TOP_TILES = TOP_NP / 16;                 // 11 tile rows
+constexpr int TOP_NT = TOP_TILES * (TOP_TILES + 1) / 2;  // 66 lower tiles
+constexpr int TOP_SLOTS = (TOP_NT + SP_WAVES - 1) / SP_WAVES;  // tiles per wave at most
+
+__global__ void __launch_bounds__(1024) ba_dense_top_kernel(BaArgs a) {
+  if (*a.done) return;
+  const int T = a.top_T, n = 7 * T;
+  const int* cols = a.top_tab + 4;
+  const int* map = cols + T;
+  __shared__ double sL[TOP_NMAX * (TOP_NMAX + 1) / 2];  // the factor, packed lower: (r, c) at r (r + 1) / 2 + c
+  __shared__ double sP[TOP_NP][8];                        // (a): the panel's columns as they stand (rows >= c0)
+  __shared__ double sPL[TOP_NP][8];                       // (c): its L, zero outside rows [c0 + 7, n) and in column 7
+  __shared__ double sy[TOP_NP];                           // rhs -> forward-substituted y -> x
+  __shared__ double sinv[TOP_NMAX];                       // 1 / L_mm
+  __shared__ int s_fail;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  // this wave's tiles u = w + 16 s (lower tiles in row order: u = I (I + 1) / 2 + J), their accumulators
+  int tI[TOP_SLOTS], tJ[TOP_SLOTS];
+  d4v acc[TOP_SLOTS];
+#pragma unroll
+  for (int q = 0; q < TOP_SLOTS; q++) {
+    const int u = w + SP_WAVES * q;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= u) I++;
+    tI[q] = u < TOP_NT ? I : -1;
+    tJ[q] = u - I * (I + 1) / 2;
+    // the dense A from the top columns' factor blocks (block (a, b) row m, column mm), upper half zero
+#pragma unroll
+    for (int r4 = 0; r4 < 4; r4++) {
+      const int r = 16 * I + lk + 4 * r4, c = 16 * tJ[q] + lr;
+      double v = 0.0;
+      if (u < TOP_NT && r < n && c <= r) {
+        const int blk = map[(r / 7) * T + c / 7];
+        if (blk >= 0) v = a.L[(size_t)blk * 64 + (r % 7) * 8 + c % 7];
+      }
+      acc[q][r4] = v;
+    }
+  }
+  for (int i = threadIdx.x; i < TOP_NP * 8; i += 1024) (&sPL[0][0])[i] = 0.0;
+  for (int r = threadIdx.x; r < TOP_NP; r += 1024) sy[r] = r < n ? a.y[(size_t)cols[r / 7] * 8 + r % 7] : 0.0;
+  if (threadIdx.x == 0) s_fail = 0;
+  for (int p = 0; p < T; p++) {
+    const int c0 = 7 * p;
+    // (a) the panel's columns [c0, c0 + 7), rows >= their diagonal, from the owning tiles
+#pragma unroll
+    for (int q = 0; q < TOP_SLOTS; q++) {
+      if (tI[q] < 0 || 16 * tJ[q] > c0 + 6 || 16 * tJ[q] + 15 < c0) continue;
+#pragma unroll
+      for (int r4 = 0; r4 < 4; r4++) {
+        const int r = 16 * tI[q] + lk + 4 * r4, c = 16 * tJ[q] + lr;
+        if (c >= c0 && c < c0 + 7 && r >= c && r < n) sP[r][c - c0] = acc[q][r4];
+      }
+    }
+    __syncthreads();  // every wave is past its (d) of the previous panel: sPL is free
+    // (b) the diagonal block (lanes 0-6: its rows, lane 7: the rhs), then L_pp, 1/L_mm and y_p into LDS
+    if (w == 0) {
+      double v[7];
+#pragma unroll
+      for (int c = 0; c < 7; c++)
+        v[c] = lane < 7 ? (c <= lane ? sP[c0 + lane][c] : 0.0) : (lane == 7 ? sy[c0 + c] : 0.0);
+      bool fail = false;
+      double inv[7];
+#pragma unroll
+      for (int m = 0; m < 7; m++) {
+        double d = bcast_lane(v[m], m);
+        if (!(d > 0.0)) {  // not positive definite: the step is discarded (dx = 0), as SimplicialLLT's info
+          fail = true;
+          d = 1.0;
+        }
+        inv[m] = rsqrt_nr(d);
+        const double l = v[m] * inv[m];
+        v[m] = lane == m ? d * inv[m] : l;
+#pragma unroll
+        for (int c = m + 1; c < 7; c++) v[c] = fma(-l, bcast_lane(l, c), v[c]);
+      }
+      if (fail && lane == 0) s_fail = 1;
+      if (lane < 7) {
+        double* row = sL + (size_t)(c0 + lane) * (c0 + lane + 1) / 2 + c0;
+#pragma unroll
+        for (int c = 0; c < 7; c++)
+          if (c <= lane) row[c] = v[c];
+        sinv[c0 + lane] = inv[0];
+#pragma unroll
+        for (int m = 1; m < 7; m++)
+          if (lane == m) sinv[c0 + lane] = inv[m];
+      } else if (lane == 7) {
+#pragma unroll
+        for (int c = 0; c < 7; c++) sy[c0 + c] = v[c];
+      }
+      if (lane < 56) sPL[c0 + lane / 8][lane % 8] = 0.0;  // the previous panel's L rows: no trailing part any more
+    }
+    __syncthreads();
+    // (c) the panel of L below the diagonal block: x L_pp^T = a per row (right-looking, as sp_rows_extra), its rhs
+    const int r = c0 + 7 + (int)threadIdx.x;
+    if (r < n) {
+      double v[7];
+#pragma unroll
+      for (int c = 0; c < 7; c++) v[c] = sP[r][c];
+#pragma unroll
+      for (int m = 0; m < 7; m++) {
+        v[m] *= sinv[c0 + m];
+#pragma unroll
+        for (int c = m + 1; c < 7; c++) v[c] = fma(-v[m], sL[(size_t)(c0 + c) * (c0 + c + 1) / 2 + c0 + m], v[c]);
+      }
+      double* row = sL + (size_t)r * (r + 1) / 2 + c0;
+      double b = sy[r];
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        row[c] = v[c];
+        sPL[r][c] = v[c];
+        b = fma(-v[c], sy[c0 + c], b);
+      }
+      sy[r] = b;
+    }
+    __syncthreads();
+    // (d) the trailing tiles: C -= P P^T (A = -P rows of tile I, B = P rows of tile J; rows outside the trailing
+    // part of P are zero, so the rest of every tile is unchanged)
+#pragma unroll
+    for (int q = 0; q < TOP_SLOTS; q++) {
+      if (tI[q] < 0 || 16 * tJ[q] + 15 < c0 + 7) continue;
+      const double a0 = -sPL[16 * tI[q] + lr][lk], a1 = -sPL[16 * tI[q] + lr][4 + lk];
+      const double b0 = sPL[16 * tJ[q] + lr][lk], b1 = sPL[16 * tJ[q] + lr][4 + lk];
+      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[q], 0, 0, 0);
+      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[q], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  // back substitution from the root: x_p = L_pp^-T z_p (wave 0), then z_c -= L(c0 + m, c) x_m for the rows before it
+  for (int p = T - 1; p >= 0; p--) {
+    const int c0 = 7 * p;
+    if (w == 0 && lane == 0) {
+      double x[7];
+#pragma unroll
+      for (int mm = 6; mm >= 0; mm--) {
+        double vv = sy[c0 + mm];
+#pragma unroll
+        for (int q = mm + 1; q < 7; q++) vv = fma(-sL[(size_t)(c0 + q) * (c0 + q + 1) / 2 + c0 + mm], x[q], vv);
+        x[mm] = vv * sinv[c0 + mm];
+      }
+#pragma unroll
+      for (int mm = 0; mm < 7; mm++) sy[c0 + mm] = x[mm];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < c0; c += 1024) {
+      double z = sy[c];
+#pragma unroll
+      for (int m = 0; m < 7; m++) z = fma(-sL[(size_t)(c0 + m) * (c0 + m + 1) / 2 + c], sy[c0 + m], z);
+      sy[c] = z;
+    }
+    __syncthreads();
+  }
+  for (int r = threadIdx.x; r < n; r += 1024) a.xs[(size_t)cols[r / 7] * 8 + r % 7] = sy[r];
+  if (threadIdx.x == 0 && s_fail) atomicOr(a.bad, BA_BAD_LLT);
+}
+
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
-__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
+__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh, int phase) {
   if (*a.done) return;
   __shared__ __attribute__((aligned(16))) int s_plan[LT ? SP_PLAN_BYTES / 4 : 4];
   __shared__ double s_red[SP_WAVES][64];  // per-wave staging: L_jk and the back-substitution sums
@@ -1509,6 +1683,15 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
       f_fac[i] = fac_init[i];
       f_xd[i] = 0;
     }
+    if (phase == 2) {  // after the dense top phase: its columns' x (a.xs) and their done flags
+      __syncthreads();
+      const int* tc = a.top_tab + 4;
+      for (int i = threadIdx.x; i < 8 * a.top_T; i += 1024) {
+        const int j = tc[i >> 3];
+        X[(size_t)j * 8 + (i & 7)] = a.xs[(size_t)j * 8 + (i & 7)];
+        if ((i & 7) == 0) f_xd[j] = 1;
+      }
+    }
   }
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
@@ -1518,7 +1701,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     // every wave walks its own task list (step order); a task waits only for its inputs
     const int* S = T.sched;
     const int2* wl = reinterpret_cast<const int2*>(S + 2 * (SP_WAVES + 1) + nb);
-    for (int t = S[w]; t < S[w + 1]; t++) {
+    for (int t = phase == 2 ? S[w + 1] : S[w]; t < S[w + 1]; t++) {
       const int2 tk = wl[t];
       if (tk.x >= 0) {
         const int j = tk.x, gp = T.pull_grp[j];
@@ -1541,6 +1724,10 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     }
     __syncthreads();
     SPST(2 + nlev);
+    if (phase == 1) {  // factor only (the dense top phase follows): report a failed pivot through *a.bad
+      if (threadIdx.x == 0 && s_bad != 0) atomicOr(a.bad, s_bad);
+      return;
+    }
     const int* bs_ptr = S + SP_WAVES + 1;
     const int* bs_col = S + 2 * (SP_WAVES + 1) + nb + 2 * S[SP_WAVES];
     for (int t = bs_ptr[w]; t < bs_ptr[w + 1]; t++) {
@@ -1575,7 +1762,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   __syncthreads();
   SPST(3 + 2 * nlev);
   // the multi-workgroup factor launches (wide steps, subtree phase, supernodal kernels) report through *a.bad
-  const int ext_bad = (a.wide_steps > 0 || a.sub_wgs > 0 || a.snode) ? *(volatile int*)a.bad : 0;
+  const int ext_bad = (a.wide_steps > 0 || a.sub_wgs > 0 || a.snode || a.top_T > 0) ? *(volatile int*)a.bad : 0;
   const bool failed = s_bad != 0 || ext_bad != 0;
   const bool stalled = ((s_bad | ext_bad) & BA_BAD_STALL) != 0;
   const int n = a.nb * 7;
@@ -1694,7 +1881,7 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
       const hipError_t e = m3s_launch_ba_snode(a, a->sn_wgs, s);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
     return hipGetLastError();
   }
   static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
@@ -1716,14 +1903,19 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l] * xs), dim3(64), 0, s, *a, step_base[l],
                          step_na[l], xs);
-  if (flow_fits)
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+  if (flow_fits && a->top_T > 0) {  // dense top phase between a factor-only and a back-substitution-only run
+    if (a->top_T > m3s::TOP_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 1);
+    hipLaunchKernelGGL(m3s::ba_dense_top_kernel, dim3(1), dim3(1024), 0, s, *a);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 2);
+  } else if (flow_fits)
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
   else if (lds <= (size_t)m3s::SP_PLAN_BYTES) {
     BaArgs b = *a;
     b.flow = 0;
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, b, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, b, K, nL, delta_thresh, 0);
   }
   else
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
   return hipGetLastError();
 }

@@ -380,7 +380,39 @@ int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vec
   return nwg;
 }
 
-double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub) {
+int ba_top_plan(const BaPattern& P, int top, std::vector<int>* tab) {
+  tab->clear();
+  if (top <= 0 || top >= P.nlev) return 0;
+  const std::vector<int> lev = col_levels(P);
+  std::vector<int> cols, pos(P.nb, -1);
+  for (int j = 0; j < P.nb; j++)
+    if (lev[j] >= top) {
+      pos[j] = (int)cols.size();
+      cols.push_back(j);
+    }
+  const int T = (int)cols.size();
+  tab->assign(4 + T + (size_t)T * T, -1);
+  int* t = tab->data();
+  t[0] = T;
+  t[1] = top;
+  t[2] = t[3] = 0;
+  for (int a = 0; a < T; a++) t[4 + a] = cols[a];
+  int* map = t + 4 + T;
+  for (int b = 0; b < T; b++) {
+    const int j = cols[b];
+    for (int q = P.col_ptr[j]; q < P.col_ptr[j + 1]; q++) {
+      const int a = pos[P.rowL[q]];
+      if (a < 0) {  // struct(j) of a top column holds only its ancestors: top columns
+        tab->clear();
+        return 0;
+      }
+      map[(size_t)a * T + b] = q;
+    }
+  }
+  return T;
+}
+
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub, int top) {
   const int nb = P.nb, nlev = P.nlev;
   sched->clear();
   if (nb <= 0) return 0.0;
@@ -396,6 +428,7 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
       if (fac_task[k] >= 0) deps.push_back(fac_task[k]);
     }
   };
+  const bool has_top = top > 0 && top < nlev;
   for (int l = std::max(0, wide); l <= nlev; l++) {
     if (l < nlev && l >= sub)
       for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
@@ -403,10 +436,19 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
         deps.clear();
         if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
         if (g >= 0) src_deps(g);
+        if (has_top && l >= top) {  // the dense top phase factors j; its pull group runs here when its sources do not
+          if (l == top && g >= 0) {
+            last_grp[j] = (int)tasks.size();
+            tasks.push_back({-1 - g, napplied[j]++});
+            F.place(deps, group_cost(P, g));
+          }
+          continue;
+        }
         fac_task[j] = (int)tasks.size();
         tasks.push_back({j, napplied[j]});
         F.place(deps, factor_cost(P, j));
       }
+    if (has_top && l - 1 >= top) continue;  // groups with top sources: the dense phase
     for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
       const int j = P.grp[4 * (size_t)t];
       if (l < sub && lev[j] < sub) continue;  // a subtree's own group: the subtree launch ran it
@@ -425,14 +467,16 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
   FlowSim B(waves, 0.15);
   std::vector<int> bcol, bwave(nb, -1), btask(nb, -1);
   for (int j = nb - 1; j >= 0; j--) {
+    if (has_top && lev[j] >= top) continue;  // solved by the dense top phase (x and its flag preset)
     deps.clear();
-    if (P.col_ptr[j + 1] - P.col_ptr[j] > 1) deps.push_back(btask[P.rowL[P.col_ptr[j] + 1]]);
+    if (P.col_ptr[j + 1] - P.col_ptr[j] > 1 && btask[P.rowL[P.col_ptr[j] + 1]] >= 0)
+      deps.push_back(btask[P.rowL[P.col_ptr[j] + 1]]);
     btask[j] = (int)bcol.size();
     bcol.push_back(j);
     bwave[j] = B.place(deps, 0.7 + 0.02 * (P.col_ptr[j + 1] - P.col_ptr[j]));
   }
   const int nt = (int)tasks.size();
-  sched->assign(2 * (waves + 1) + nb + 2 * (size_t)nt + nb, 0);
+  sched->assign(2 * (waves + 1) + nb + 2 * (size_t)nt + bcol.size(), 0);
   int* wl_ptr = sched->data();
   int* bs_ptr = wl_ptr + waves + 1;
   int* fac_init = bs_ptr + waves + 1;

@@ -63,8 +63,18 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P,
 #define BA_BS_COL 0xFFFFFF
 // sub > 0 (subtree phase below, wide = 0): steps [0, sub) belong to the subtree launch except their update groups
 // whose target column sits at level >= sub, which the one-workgroup schedule runs first (in step order per target).
+// top > 0 (dense top phase, ba_top_plan): the columns at levels >= top are factored and solved by ba_dense_top_kernel
+// between a factor-only and a back-substitution-only run of the one-workgroup kernel: their factor tasks, the update
+// groups whose sources sit at levels >= top and their back-substitution tasks leave the lists; the pull groups of the
+// columns at level `top` (sources below the cut) become update-group tasks.
 // Returns the simulated finish time (us) of the factor part (the cost model's estimate).
-double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub = 0);
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub = 0, int top = 0);
+
+// Dense top phase (ba_dense_top_kernel, ba.hip): the columns at elimination-tree levels >= `top` (an ancestor-closed
+// set: the root end of the tree, where the factor is nearly dense) as one dense (7T x 7T) fp64 Cholesky on the matrix
+// cores in one workgroup. Layout (ints): [T, top, 0, 0] [top columns ascending (T)] [T x T: the factor block of
+// L(row top_col[a], column top_col[b]) for a >= b, or -1 where the pattern has none]. Returns T (0: no top phase).
+int ba_top_plan(const BaPattern& P, int top, std::vector<int>* tab);
 
 // Subtree phase (ba_subtree_kernel, ba.hip): the columns below elimination-tree level `cut` fall into independent
 // subtrees (a column belongs to its highest ancestor below the cut). One workgroup per subtree (small subtrees

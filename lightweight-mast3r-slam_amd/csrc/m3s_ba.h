@@ -105,6 +105,8 @@ struct BaArgs {
   const int* sn_tab;  // supernodal factorisation (ba_pattern.h ba_snode_plan), or null
   int snode;          // the factor ran in ba_snode_kernel (the factor kernel then only substitutes back)
   int sn_wgs;         // its multi-workgroup launch's workgroups
+  const int* top_tab;  // dense top phase (ba_pattern.h ba_top_plan), or null
+  int top_T;           // its poses (0: none)
   int* stalled;  // sticky: a dataflow / LDS hand-off wait timed out in some solve of this plan (M3S_ESTALL)
   int force_stall;  // tests only (M3S_BA_FORCE_STALL): the dataflow waits are never satisfied
 };

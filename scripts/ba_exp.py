@@ -61,14 +61,14 @@ for rep in range(2):
         out[name] = ms.value / max(cnt.value, 1)
     import hashlib
     twc_hash = hashlib.sha1(Twc.cpu().numpy().tobytes()).hexdigest()[:12]
-    info = (ctypes.c_int * 12)()
+    info = (ctypes.c_int * 13)()
     _lib.check(lib.m3s_ba_plan_info(ctypes.byref(shard.plan), info))
     # the linearisation's compulsory bytes per launch (bench.py ba roofline): 16 B record per point and
     # edge + 12 B X_j per point and target keyframe + 17 partial / edge-sum rows of 288 B per edge
     gb = (16 * H * W * E + 12 * H * W * info[5] + 17 * 288 * E) / 1e6  # MB -> MB/ms = GB/s
     print(f"rep {rep}: Twc sha1 {twc_hash} E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
           f"compulsory)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}  wide steps {info[3]}, subtree "
-          f"steps {info[8]} in {info[9]} workgroups, of {info[2]} levels", flush=True)
+          f"steps {info[8]} in {info[9]} workgroups, of {info[2]} levels, dense top {info[12]} poses", flush=True)
 
 
 if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the last factor launch
@@ -94,7 +94,7 @@ if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the la
     print("back (level: us since the previous barrier):", " ".join(segs))
     # dataflow build (flow schedule): per-task wait-done / end stamps of the factor lists, per-column end stamps of
     # the back substitution; per wave the time spent waiting vs working, and the wave-0 timeline
-    info = (ctypes.c_int * 12)()
+    info = (ctypes.c_int * 13)()
     _lib.check(lib.m3s_ba_plan_info(ctypes.byref(shard.plan), info))
     if os.environ.get("M3S_BA_FLOW", "1") != "0" and buf[1000] != 0:
         ts = [(buf[1000 + k] - buf[0]) / 100.0 for k in range(2000)]
