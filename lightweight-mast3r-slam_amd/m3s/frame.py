@@ -244,6 +244,33 @@ class SharedKeyframes:
             return self.K
 
 
+_SLOT_BUFFERS = ("dataset_idx", "img", "uimg", "img_shape", "img_true_shape", "T_WC", "X", "C", "N", "N_updates",
+                 "feat", "pos", "is_dirty", "K")
+
+
+def slot_frame(store, idx):
+    """store[idx] of a buffer-backed keyframe store (this module's SharedKeyframes or the reference's,
+    frame.py:248-267) for a caller that already holds store.lock: the same record of slot views, with the three
+    scalar reads (dataset_idx, N, N_updates: int(...) on device tensors, one synchronising D2H copy each in
+    __getitem__) done as ONE copy, and without __getitem__'s own (nested, one Manager round trip per acquire and
+    release) lock hold. None when the store is not buffer-backed."""
+    if not all(torch.is_tensor(getattr(store, a, None)) for a in _SLOT_BUFFERS):
+        return None
+    if not all(getattr(store, a).dtype == torch.int32 for a in ("dataset_idx", "N", "N_updates")):
+        return None
+    fid, n, nu = torch.stack((store.dataset_idx[idx], store.N[idx], store.N_updates[idx])).tolist()
+    kf = Frame(fid, (store.h, store.w), T_WC=Sim3(store.T_WC[idx]))
+    kf.img, kf.uimg = store.img[idx], store.uimg[idx]
+    kf.img_shape, kf.img_true_shape = store.img_shape[idx], store.img_true_shape[idx]
+    kf.X_canon, kf.C = store.X[idx], store.C[idx]
+    kf.feat, kf.pos = store.feat[idx], store.pos[idx]
+    kf.N, kf.N_updates = n, nu
+    kf.shared = True
+    if config["use_calib"]:
+        kf.K = store.K
+    return kf
+
+
 def slot_rows(store, keyframe, idx):
     """(X row, C row, N, N_updates, is_dirty) device views of slot idx of a buffer-backed keyframe store (this
     module's SharedKeyframes or the reference's, frame.py:220-245) when `keyframe` is that slot's record (its X_canon

@@ -17,7 +17,7 @@ import torch
 
 from m3s import _lib
 from m3s.config import config
-from m3s.frame import Frame, slot_rows
+from m3s.frame import Frame, slot_frame, slot_rows
 from m3s.matching import match, match_halves
 from m3s.sim3 import Sim3
 
@@ -211,13 +211,17 @@ class FrameTracker:
         (main.py), so the index read with the keyframe is the one len() would return at the write-back. A
         lock-guarded store (the reference's SharedKeyframes, frame.py:220-327: every Manager lock and Value access
         is an IPC) is read under one lock hold: n_size once, then the slot, instead of last_keyframe()'s two n_size
-        reads plus a separate len()."""
+        reads plus a separate len(); a buffer-backed slot is read inside that hold (slot_frame: no nested lock, one
+        D2H copy for its three scalars instead of three)."""
         kfs = self.keyframes
         lock, n_size = getattr(kfs, "lock", None), getattr(kfs, "n_size", None)
         if lock is not None and n_size is not None and hasattr(n_size, "value"):
             with lock:
                 n = n_size.value
-                return (kfs[n - 1], n - 1) if n > 0 else (None, -1)
+                if n <= 0:
+                    return None, -1
+                kf = slot_frame(kfs, n - 1)
+                return (kfs[n - 1] if kf is None else kf), n - 1
         n = len(kfs)
         return (kfs[n - 1], n - 1) if n > 0 else (None, -1)
 

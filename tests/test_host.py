@@ -155,6 +155,49 @@ def test_frame_owned_pointmap_is_copied_before_in_place_modes():
         config["tracking"]["filtering_mode"] = mode
 
 
+@pytest.mark.parametrize("use_calib", [False, True])
+def test_slot_frame_is_the_store_record(use_calib):
+    """FrameTracker._last_keyframe reads a buffer-backed store's last slot inside its one lock hold (slot_frame): the
+    same record SharedKeyframes.__getitem__ returns (frame.py:248-267), views of the same slot rows and the same
+    scalars, without the nested lock and with one scalar copy instead of three."""
+    import multiprocessing as mp
+
+    from m3s.config import config
+    from m3s.frame import Frame, SharedKeyframes, slot_frame
+    from m3s.sim3 import Sim3
+    from m3s.tracker import FrameTracker
+
+    H, W = 16, 32
+    g = torch.Generator().manual_seed(5)
+    manager = mp.get_context("spawn").Manager()
+    config["use_calib"] = use_calib
+    try:
+        kfs = SharedKeyframes(manager, H, W, buffer=4, device="cpu", feat_dim=8)
+        for fid in (7, 9):
+            kf = Frame(fid, (H, W), T_WC=Sim3(torch.randn(1, 8, generator=g)))
+            kf.update_pointmap(torch.randn(H * W, 3, generator=g), torch.rand(H * W, 1, generator=g) + 1)
+            kf.update_pointmap(torch.randn(H * W, 3, generator=g), torch.rand(H * W, 1, generator=g) + 1)
+            kf.img, kf.uimg = torch.rand(3, H, W, generator=g), torch.rand(H, W, 3, generator=g)
+            kf.img_shape = torch.tensor([[H, W]], dtype=torch.int)
+            kf.img_true_shape = kf.img_shape.clone()
+            kf.feat = torch.rand(1, H * W // 256, 8, generator=g)
+            kf.pos = torch.randint(0, 9, (1, H * W // 256, 2), generator=g)
+            kfs.append(kf)
+        ref, got = kfs[1], slot_frame(kfs, 1)
+        assert (got.frame_id, got.N, got.N_updates) == (ref.frame_id, ref.N, ref.N_updates) == (9, 2, 2)
+        assert all(type(v) is int for v in (got.frame_id, got.N, got.N_updates))
+        for a in ("img", "uimg", "img_shape", "img_true_shape", "X_canon", "C", "feat", "pos"):
+            assert getattr(got, a).data_ptr() == getattr(ref, a).data_ptr(), a
+        assert got.T_WC.data.data_ptr() == ref.T_WC.data.data_ptr() and got.shared
+        assert (got.K is kfs.K) if use_calib else got.K is None
+        kf, idx = FrameTracker(None, kfs, "cpu")._last_keyframe()
+        assert idx == 1 and kf.frame_id == 9 and kf.X_canon.data_ptr() == kfs.X[1].data_ptr()
+        assert slot_frame([], 0) is None  # not buffer-backed: the tracker falls back to store[idx]
+    finally:
+        config["use_calib"] = False
+        manager.shutdown()
+
+
 def test_synthetic_pair_is_consistent():
     from m3s.sim3 import Sim3
     from m3s.synthetic import make_pair
