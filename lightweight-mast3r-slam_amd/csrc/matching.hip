@@ -20,16 +20,23 @@ namespace m3s {
 
 // Refine tile path: D11 (B,H,W,24) f32 -> f16 (RNE, == torch .half()) of pixel n into image b's three chunk planes
 // (H,W,8) (one 16-B store per plane: lanes store consecutive pixels); returns the sum of squares of its f16 values
-// (the refine screen's norm bound, refine.hip; 0 past the image)
-__device__ __forceinline__ float desc_planar(const float* __restrict__ D11, h1* __restrict__ D11h, int b, int n, int N) {
+// (the refine screen's norm bound, refine.hip; 0 past the image). The loads are split from the conversion so the
+// prep kernel issues them first, under the ray halo's loads and stencil (desc_load, then desc_planar).
+// (unconditional: a pixel past the image loads pixel N - 1 and stores nothing, so no branch join waits on the loads)
+__device__ __forceinline__ void desc_load(const float* __restrict__ D11, int b, int n, int N, float4 v[6]) {
+  const float4* src = reinterpret_cast<const float4*>(D11 + ((size_t)b * N + min(n, N - 1)) * 24);
+#pragma unroll
+  for (int k = 0; k < 6; k++) v[k] = src[k];
+}
+
+__device__ __forceinline__ float desc_planar(const float4 v[6], h1* __restrict__ D11h, int b, int n, int N) {
   float ss = 0.0f;
   if (n < N) {
-    const float4* src = reinterpret_cast<const float4*>(D11 + ((size_t)b * N + n) * 24);
     const size_t plane = (size_t)N * 8;
     h1* dst = D11h + (size_t)b * 3 * plane + (size_t)n * 8;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      const float4 v0 = src[2 * c], v1 = src[2 * c + 1];
+      const float4 v0 = v[2 * c], v1 = v[2 * c + 1];
       h1 r[8] = {(h1)v0.x, (h1)v0.y, (h1)v0.z, (h1)v0.w, (h1)v1.x, (h1)v1.y, (h1)v1.z, (h1)v1.w};
       *reinterpret_cast<uint4*>(dst + c * plane) = *reinterpret_cast<uint4*>(r);
 #pragma unroll
@@ -47,6 +54,10 @@ __device__ __forceinline__ float desc_planar(const float* __restrict__ D11, h1* 
 // the (B,H,W,F) layout of the per-pixel refine kernels.
 // ------------------------------------------------------------------------------------------
 #define PREP_T 16
+// DMODE: 0 no descriptors, 1 planar (refine tile path), 2 the (B,H,W,F) row layout; a template argument so the
+// planar path's descriptor loads, issued first, cross no branch join (a runtime `if` made the compiler convert them,
+// and so wait for them, right behind the loads)
+template <int DMODE>
 __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict__ X11, float* __restrict__ rays9,
                                                         const float* __restrict__ D11, h1* __restrict__ D11h, int H,
                                                         int W, int F, int planar, float* __restrict__ cnorm_part) {
@@ -54,24 +65,44 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
   const int b = blockIdx.z;
   const int u0 = blockIdx.x * PREP_T, v0 = blockIdx.y * PREP_T;
   const float* Xb = X11 + (size_t)b * H * W * 3;
-  for (int t = threadIdx.x; t < (PREP_T + 2) * (PREP_T + 2); t += blockDim.x) {
-    const int ly = t / (PREP_T + 2), lx = t % (PREP_T + 2);
-    int y = v0 + ly - 1, x = u0 + lx - 1;
-    // reflect padding (F.pad mode="reflect"): -1 -> 1, H -> H-2
-    y = y < 0 ? -y : (y >= H ? 2 * H - 2 - y : y);
-    x = x < 0 ? -x : (x >= W ? 2 * W - 2 - x : x);
-    y = min(max(y, 0), H - 1);
-    x = min(max(x, 0), W - 1);
-    const float* p = Xb + ((size_t)y * W + x) * 3;
-    const float a = p[0], c = p[1], d = p[2];
-    const float n = fmaxf(sqrtf(a * a + c * c + d * d), 1e-12f);
-    tile[t * 3 + 0] = a / n;
-    tile[t * 3 + 1] = c / n;
-    tile[t * 3 + 2] = d / n;
-  }
-  __syncthreads();
   const int lx = threadIdx.x % PREP_T, ly = threadIdx.x / PREP_T;
   const int x = u0 + lx, y = v0 + ly;
+  constexpr bool planar_d = DMODE == 1;
+  const int dn = (x < W && y < H) ? y * W + x : H * W;
+  // the 18x18 halo: 324 pixels, two per thread at most (256 threads); both loads issued before either is used
+  constexpr int HALO = (PREP_T + 2) * (PREP_T + 2);
+  static_assert(HALO <= 2 * 256, "prep halo: two pixels per thread");
+  float hv[2][3];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int t = min((int)threadIdx.x + 256 * r, HALO - 1);
+    const int hy = t / (PREP_T + 2), hx = t % (PREP_T + 2);
+    int yy = v0 + hy - 1, xx = u0 + hx - 1;
+    // reflect padding (F.pad mode="reflect"): -1 -> 1, H -> H-2
+    yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+    xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+    yy = min(max(yy, 0), H - 1);
+    xx = min(max(xx, 0), W - 1);
+    const float* p = Xb + ((size_t)yy * W + xx) * 3;
+    hv[r][0] = p[0];
+    hv[r][1] = p[1];
+    hv[r][2] = p[2];
+  }
+  // then the pixel's descriptor loads (vmcnt retires in order: behind the halo's, so the stencil waits only for those)
+  float4 dv[6];
+  if constexpr (planar_d) desc_load(D11, b, dn, H * W, dv);
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int t = threadIdx.x + 256 * r;
+    if (t < HALO) {
+      const float a = hv[r][0], c = hv[r][1], d = hv[r][2];
+      const float n = fmaxf(sqrtf(a * a + c * c + d * d), 1e-12f);
+      tile[t * 3 + 0] = a / n;
+      tile[t * 3 + 1] = c / n;
+      tile[t * 3 + 2] = d / n;
+    }
+  }
+  __syncthreads();
   if (x < W && y < H) {
     float* o = rays9 + (((size_t)b * H + y) * W + x) * 9;
 #define T3(dy, dx, c) tile[(((ly + 1 + (dy)) * (PREP_T + 2)) + (lx + 1 + (dx))) * 3 + (c)]
@@ -88,8 +119,8 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
     }
 #undef T3
   }
-  if (D11 != nullptr && planar) {
-    const float ss = desc_planar(D11, D11h, b, (x < W && y < H) ? y * W + x : H * W, H * W);
+  if constexpr (planar_d) {
+    const float ss = desc_planar(dv, D11h, b, dn, H * W);
     if (cnorm_part != nullptr) {
       // the tile's max |D11h[pixel]|_2, one partial per block (proj_occlusion reduces them before refine reads the
       // bound); NaN / inf descriptors give a NaN / inf partial, which switches the screen off for every lane
@@ -103,9 +134,9 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
         cnorm_part[((size_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
             fmaxf_nan(fmaxf_nan(s_max[0], s_max[1]), fmaxf_nan(s_max[2], s_max[3]));
     }
-  } else if (D11 != nullptr) {
+  } else if constexpr (DMODE == 2) {
     // f32 -> f16 of this tile's descriptor rows (B,H,W,F), 4 channels per lane-step (the per-pixel kernels'
-    // layout; the refine tile path's planar layout is written by the proj launch, desc_planar below)
+    // layout; the refine tile path's planar layout is written by the proj launch, desc_planar above)
     for (int t = threadIdx.x; t < PREP_T * PREP_T * (F / 4); t += blockDim.x) {
       const int pix = t / (F / 4), q = t % (F / 4);
       const int xx = u0 + pix % PREP_T, yy = v0 + pix / PREP_T;
@@ -411,8 +442,9 @@ __global__ void __launch_bounds__(256) refine_f32_kernel(const float* __restrict
 extern "C" hipError_t m3s_launch_prep(const float* X11, float* rays9, const float* D11, void* D11h, int B, int H,
                                       int W, int F, int planar, float* cnorm_part, hipStream_t s) {
   dim3 grid((W + PREP_T - 1) / PREP_T, (H + PREP_T - 1) / PREP_T, B);
-  hipLaunchKernelGGL(m3s::prep_rays_kernel, grid, dim3(256), 0, s, X11, rays9, D11,
-                     reinterpret_cast<m3s::h1*>(D11h), H, W, F, planar, cnorm_part);
+  auto k = D11 == nullptr ? m3s::prep_rays_kernel<0> : planar ? m3s::prep_rays_kernel<1> : m3s::prep_rays_kernel<2>;
+  hipLaunchKernelGGL(k, grid, dim3(256), 0, s, X11, rays9, D11, reinterpret_cast<m3s::h1*>(D11h), H, W, F, planar,
+                     cnorm_part);
   return hipGetLastError();
 }
 
