@@ -180,76 +180,166 @@ __device__ __forceinline__ void bilin_w(float u, float v, int& u11, int& v11, fl
   w[3] = cu * cv;
 }
 
-template <int NC>
-__device__ __forceinline__ void bilin_sample(const float* __restrict__ img, int W, int u11, int v11, const float w[4],
-                                             float* out) {
-  const float* r11 = img + ((size_t)(v11 + 1) * W + (u11 + 1)) * 9;
-  const float* r12 = img + ((size_t)(v11 + 1) * W + u11) * 9;
-  const float* r21 = img + ((size_t)v11 * W + (u11 + 1)) * 9;
-  const float* r22 = img + ((size_t)v11 * W + u11) * 9;
+// The four corners' 9 channels: channels 0..7 as four packed fp32 pairs (each element rounds as the scalar
+// expression w0 r11 + w1 r12 + w2 r21 + w3 r22 does: -ffp-contract=off, no fma; the loads land in even-aligned
+// register pairs and the weights broadcast by op_sel, so no moves), channel 8 scalar
+__device__ __forceinline__ void bilin_sample9(const float* __restrict__ img, int W, int u11, int v11, const float w[4],
+                                              float* out) {
+  typedef float wf2 __attribute__((ext_vector_type(2)));
+  // two 18-float runs, (v11, u11 .. u11 + 1) and the row below, from one 32-bit offset each (u11, v11 lie inside the
+  // image and the launchers require 9 H W < 2^31): the corners are immediate offsets of the two run pointers
+  const unsigned o = (unsigned)(v11 * W + u11) * 9u;
+  const float* r22 = img + o;
+  const float* r21 = r22 + 9;
+  const float* r12 = img + (o + 9u * (unsigned)W);
+  const float* r11 = r12 + 9;
+  const wf2 w0 = {w[0], w[0]}, w1 = {w[1], w[1]}, w2 = {w[2], w[2]}, w3 = {w[3], w[3]};
+  auto ld2 = [](const float* q) {
+    wf2 r;
+    r.x = q[0];
+    r.y = q[1];
+    return r;
+  };
 #pragma unroll
-  for (int j = 0; j < NC; j++) out[j] = w[0] * r11[j] + w[1] * r12[j] + w[2] * r21[j] + w[3] * r22[j];
+  for (int j = 0; j < 8; j += 2) {
+    const wf2 o = w0 * ld2(r11 + j) + w1 * ld2(r12 + j) + w2 * ld2(r21 + j) + w3 * ld2(r22 + j);
+    out[j] = o.x;
+    out[j + 1] = o.y;
+  }
+  out[8] = w[0] * r11[8] + w[1] * r12[8] + w[2] * r21[8] + w[3] * r22[8];
 }
 
+// One LM iteration (matching_kernels.cu:185-270 loop body) on the carried state. LAST (the fused kernel's final
+// iteration): the occlusion test's X11 gather at both possible final pixels, the accepted step's and the kept one's,
+// is issued beside the iteration's own sample, so its round trip is not one more link after the loop; xo gets the
+// one the accept / reject picks (matching.py:68-76 reads X11 at the final .long() pixel).
+struct LmState {
+  float u, v, lambda, cost, e0, e1, e2;
+  float s[9];
+  bool conv;
+};
+
+template <bool LAST>
+__device__ __forceinline__ void lm_iter(LmState& m, const float* __restrict__ img, int H, int W, const float p[3],
+                                        float cost_thresh, const float* __restrict__ X11b, float* xo) {
+  const float* s = m.s;
+  float A00 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
+  const float A01 = s[3] * s[6] + s[4] * s[7] + s[5] * s[8];
+  float A11 = s[6] * s[6] + s[7] * s[7] + s[8] * s[8];
+  const float b0 = -(m.e0 * s[3] + m.e1 * s[4] + m.e2 * s[5]);
+  const float b1 = -(m.e0 * s[6] + m.e1 * s[7] + m.e2 * s[8]);
+  A00 += m.lambda;
+  A11 += m.lambda;
+  const float det_inv = 1.0f / (A00 * A11 - A01 * A01);
+  float u_new = m.u + det_inv * (A11 * b0 - A01 * b1);
+  float v_new = m.v + det_inv * (-A01 * b0 + A00 * b1);
+  u_new = fminf(fmaxf(u_new, 1.0f), (float)(W - 2));
+  v_new = fminf(fmaxf(v_new, 1.0f), (float)(H - 2));
+  float xa[3], xb[3];
+  if constexpr (LAST) {
+    const float* qa = X11b + ((size_t)(int)v_new * W + (int)u_new) * 3;  // .long() truncation; u, v >= 1
+    const float* qb = X11b + ((size_t)(int)m.v * W + (int)m.u) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      xa[c] = qa[c];
+      xb[c] = qb[c];
+    }
+  }
+  int u11, v11;
+  float w[4], t[9];
+  bilin_w(u_new, v_new, u11, v11, w);
+  bilin_sample9(img, W, u11, v11, w, t);
+  const float r_norm_inv = 1.0f / sqrtf(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+  const float f0 = t[0] * r_norm_inv - p[0];
+  const float f1 = t[1] * r_norm_inv - p[1];
+  const float f2 = t[2] * r_norm_inv - p[2];
+  const float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
+  if (new_cost < m.cost) {
+    m.u = u_new;
+    m.v = v_new;
+#pragma unroll
+    for (int k = 0; k < 9; k++) m.s[k] = t[k];
+    m.e0 = f0;
+    m.e1 = f1;
+    m.e2 = f2;
+    m.conv = new_cost < cost_thresh;
+    m.cost = new_cost;
+    m.lambda = (float)((double)m.lambda * 0.1);
+    if constexpr (LAST) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) xo[c] = xa[c];
+    }
+  } else {
+    m.lambda = (float)((double)m.lambda * 10.0);
+    m.conv = m.cost < cost_thresh;
+    if constexpr (LAST) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) xo[c] = xb[c];
+    }
+  }
+}
+
+// OCC: X11b non-null, xo gets X11 at the final (.long()) pixel, gathered during the last iteration (lm_iter<true>)
+template <bool OCC>
 __device__ __forceinline__ void iter_proj_point(const float* __restrict__ img, int H, int W, const float p[3],
                                                 float& u, float& v, bool& conv, int max_iter, float lambda_init,
-                                                float cost_thresh) {
-  u = fminf(fmaxf(u, 1.0f), (float)(W - 2));
-  v = fminf(fmaxf(v, 1.0f), (float)(H - 2));
-  float lambda = lambda_init;
+                                                float cost_thresh, const float* __restrict__ X11b = nullptr,
+                                                float* xo = nullptr) {
+  LmState m;
+  m.u = fminf(fmaxf(u, 1.0f), (float)(W - 2));
+  m.v = fminf(fmaxf(v, 1.0f), (float)(H - 2));
+  m.lambda = lambda_init;
+  m.conv = conv;
   // The reference samples (u, v) at the top of every iteration and (u_new, v_new) for the new cost.
   // The top-of-loop sample always equals the previous iteration's accepted sample (u_new) or its own
   // previous value (rejected), so the 9-channel sample is carried instead of refetched: one
   // dependent gather per iteration instead of two, identical values.
   int u11, v11;
-  float w[4], s[9];
-  bilin_w(u, v, u11, v11, w);
-  bilin_sample<9>(img, W, u11, v11, w, s);
+  float w[4];
+  if constexpr (OCC) {
+    if (max_iter <= 0) {  // no iteration: the occlusion pixel is the clamped start, gathered beside its sample
+      const float* q = X11b + ((size_t)(int)m.v * W + (int)m.u) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; c++) xo[c] = q[c];
+    }
+  }
+  bilin_w(m.u, m.v, u11, v11, w);
+  bilin_sample9(img, W, u11, v11, w, m.s);
   // The residual e and cost of the carried sample are carried too: an accepted step's (f, new_cost)
   // are exactly what the next iteration would recompute from the same sample (bit-identical).
   // 1.0/r_norm in double then float == IEEE float division (53 >= 2*24+2, innocuous double rounding)
-  float r_norm_inv = 1.0f / sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
-  float e0 = s[0] * r_norm_inv - p[0];
-  float e1 = s[1] * r_norm_inv - p[1];
-  float e2 = s[2] * r_norm_inv - p[2];
-  float cost = e0 * e0 + e1 * e1 + e2 * e2;
-  for (int i = 0; i < max_iter; i++) {
-    float A00 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
-    const float A01 = s[3] * s[6] + s[4] * s[7] + s[5] * s[8];
-    float A11 = s[6] * s[6] + s[7] * s[7] + s[8] * s[8];
-    const float b0 = -(e0 * s[3] + e1 * s[4] + e2 * s[5]);
-    const float b1 = -(e0 * s[6] + e1 * s[7] + e2 * s[8]);
-    A00 += lambda;
-    A11 += lambda;
-    const float det_inv = 1.0f / (A00 * A11 - A01 * A01);
-    float u_new = u + det_inv * (A11 * b0 - A01 * b1);
-    float v_new = v + det_inv * (-A01 * b0 + A00 * b1);
-    u_new = fminf(fmaxf(u_new, 1.0f), (float)(W - 2));
-    v_new = fminf(fmaxf(v_new, 1.0f), (float)(H - 2));
-    bilin_w(u_new, v_new, u11, v11, w);
-    float t[9];
-    bilin_sample<9>(img, W, u11, v11, w, t);
-    r_norm_inv = 1.0f / sqrtf(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
-    const float f0 = t[0] * r_norm_inv - p[0];
-    const float f1 = t[1] * r_norm_inv - p[1];
-    const float f2 = t[2] * r_norm_inv - p[2];
-    const float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
-    if (new_cost < cost) {
-      u = u_new;
-      v = v_new;
-#pragma unroll
-      for (int k = 0; k < 9; k++) s[k] = t[k];
-      e0 = f0;
-      e1 = f1;
-      e2 = f2;
-      conv = new_cost < cost_thresh;
-      cost = new_cost;
-      lambda = (float)((double)lambda * 0.1);
-    } else {
-      lambda = (float)((double)lambda * 10.0);
-      conv = cost < cost_thresh;
-    }
+  const float r_norm_inv = 1.0f / sqrtf(m.s[0] * m.s[0] + m.s[1] * m.s[1] + m.s[2] * m.s[2]);
+  m.e0 = m.s[0] * r_norm_inv - p[0];
+  m.e1 = m.s[1] * r_norm_inv - p[1];
+  m.e2 = m.s[2] * r_norm_inv - p[2];
+  m.cost = m.e0 * m.e0 + m.e1 * m.e1 + m.e2 * m.e2;
+  if constexpr (OCC) {
+    for (int i = 0; i < max_iter - 1; i++) lm_iter<false>(m, img, H, W, p, cost_thresh, nullptr, nullptr);
+    if (max_iter > 0) lm_iter<true>(m, img, H, W, p, cost_thresh, X11b, xo);
+  } else {
+    for (int i = 0; i < max_iter; i++) lm_iter<false>(m, img, H, W, p, cost_thresh, nullptr, nullptr);
   }
+  u = m.u;
+  v = m.v;
+  conv = m.conv;
+}
+
+// lin_to_pixel (matching.py:18-22) with Python floor semantics for any i0 sign; 32-bit division for the indices
+// inside [0, 2^31) (the same quotient and remainder)
+__device__ __forceinline__ void lin_to_pixel_f(int64_t i0, int W, float& u, float& v) {
+  if (i0 >= 0 && i0 <= 0x7fffffff) {
+    const unsigned q = (unsigned)i0 / (unsigned)W;
+    u = (float)((unsigned)i0 - q * (unsigned)W);
+    v = (float)q;
+    return;
+  }
+  int64_t vq = i0 / W, uq = i0 % W;
+  if (uq < 0) {
+    uq += W;
+    vq -= 1;
+  }
+  u = (float)uq;
+  v = (float)vq;
 }
 
 // Reference-signature kernel: rays (B,H,W,9), pts (B,N,3) normalised, p_init (B,N,2) f32.
@@ -264,7 +354,7 @@ __global__ void __launch_bounds__(256) iter_proj_kernel(const float* __restrict_
   const float p[3] = {pts[bn * 3 + 0], pts[bn * 3 + 1], pts[bn * 3 + 2]};
   float u = p_init[bn * 2 + 0], v = p_init[bn * 2 + 1];
   bool conv = false;
-  iter_proj_point(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh);
+  iter_proj_point<false>(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh);
   p_new[bn * 2 + 0] = u;
   p_new[bn * 2 + 1] = v;
   converged[bn] = conv;
@@ -289,18 +379,13 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
   const float x = X21[bn * 3 + 0], y = X21[bn * 3 + 1], z = X21[bn * 3 + 2];
   const float nrm = fmaxf(sqrtf(x * x + y * y + z * z), 1e-12f);
   const float p[3] = {x / nrm, y / nrm, z / nrm};
-  const int64_t i0 = idx_init != nullptr ? idx_init[bn] : (int64_t)n;
-  // lin_to_pixel (matching.py:18-22) with Python floor semantics for any i0 sign
-  int64_t vq = i0 / W, uq = i0 % W;
-  if (uq < 0) {
-    uq += W;
-    vq -= 1;
-  }
-  float u = (float)uq, v = (float)vq;
+  float u, v;
+  lin_to_pixel_f(idx_init != nullptr ? idx_init[bn] : (int64_t)n, W, u, v);
   bool conv = false;
-  iter_proj_point(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh);
+  float Xg[3];  // X11 at the final pixel, gathered during the last LM iteration
+  iter_proj_point<true>(rays + (size_t)b * H * W * 9, H, W, p, u, v, conv, max_iter, lambda_init, cost_thresh,
+                        X11 + (size_t)b * H * W * 3, Xg);
   const int pu = (int)u, pv = (int)v;  // .long() truncation; u,v >= 1 after clamping
-  const float* Xg = X11 + (((size_t)b * H + pv) * W + pu) * 3;
   const float dx = Xg[0] - x, dy = Xg[1] - y, dz = Xg[2] - z;
   const float d = sqrtf(dx * dx + dy * dy + dz * dz);
   p1[bn * 2 + 0] = pu;
@@ -455,6 +540,7 @@ extern "C" int m3s_prep_parts(int B, int H, int W) {
 extern "C" hipError_t m3s_launch_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
                                            uint8_t* conv, int B, int H, int W, int N, int max_iter, float lambda_init,
                                            float cost_thresh, hipStream_t s) {
+  if ((size_t)9 * H * W >= ((size_t)1 << 31)) return hipErrorInvalidValue;  // bilin_sample9's 32-bit offsets
   dim3 grid((N + 255) / 256, B);
   hipLaunchKernelGGL(m3s::iter_proj_kernel, grid, dim3(256), 0, s, rays, pts, p_init, p_new, conv, H, W, N,
                      max_iter, lambda_init, cost_thresh);
@@ -466,6 +552,7 @@ extern "C" hipError_t m3s_launch_proj_occlusion(const float* rays, const float* 
                                                 int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
                                                 int* zero_counter, const float* cnorm_part, int nparts, float* cmax,
                                                 hipStream_t s) {
+  if ((size_t)9 * H * W >= ((size_t)1 << 31)) return hipErrorInvalidValue;  // bilin_sample9's 32-bit offsets
   // cmax (nullable): one wave reduces prep's tile partials into the refine screen's bound
   dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(m3s::proj_occlusion_kernel, grid, dim3(256), 0, s, rays, X11, X21, idx_init, p1, valid, H, W,
