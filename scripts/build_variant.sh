@@ -7,7 +7,7 @@ make -s -j8 >/dev/null
 mkdir -p ../lib/exp build/exp
 HIPCC=/opt/rocm/bin/hipcc
 $HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -ffp-contract=off -fno-slp-vectorize $2 -c refine.hip -o build/exp/refine_$1.o
-$HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $2 -c track.hip -o build/exp/track_$1.o
+$HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -ffp-contract=off -fno-slp-vectorize $2 -c track.hip -o build/exp/track_$1.o
 $HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -ffp-contract=off $2 -c ba.hip -o build/exp/ba_$1.o
 $HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off $2 -c retrieval.hip -o build/exp/retrieval_$1.o
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o ../lib/exp/libm3s_$1.so build/matching.o build/exp/refine_$1.o build/exp/track_$1.o build/exp/ba_$1.o build/ba_dense.o build/peaks.o build/exp/retrieval_$1.o build/ba_pattern.o build/abi.o
