@@ -152,10 +152,19 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
 
 // max of the prep partials into cmax[0] (the refine screen's descriptor-norm bound), by the first wave of one block
 // of the launch between prep and refine (proj_occlusion)
+// (16 loads per lane in flight at once: one at a time, the 1024 partials of a 512x512 image were 16 dependent
+// round trips in front of block 0's own pixels, and the launch ends with its last block; the max is
+// order-independent, NaN included, so the result is the same)
 __device__ __forceinline__ void reduce_cnorm(const float* __restrict__ part, int nparts, float* __restrict__ cmax) {
   const int lane = threadIdx.x & 63;
   float m = 0.0f;
-  for (int i = lane; i < nparts; i += 64) m = fmaxf_nan(m, part[i]);
+  for (int base = lane; base < nparts; base += 64 * 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = part[min(base + 64 * k, nparts - 1)];
+#pragma unroll
+    for (int k = 0; k < 16; k++) m = fmaxf_nan(m, v[k]);
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf_nan(m, __shfl_xor(m, off, 64));
   if (lane == 0) *cmax = m;
