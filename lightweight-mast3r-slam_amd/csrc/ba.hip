@@ -630,8 +630,18 @@ __global__ void __launch_bounds__(64) ba_edge_kernel(BaArgs a, BaParams p, int E
   __shared__ double s_L[7][7], s_v[7], s_A[7][7], s_AL[7][7];
   const int t = threadIdx.x;
   if (t < 35) {
+    // the chunk partials in chunk order, eight loads in flight at a time (one at a time they were a chain of
+    // dependent round trips per edge); clamped loads past the last chunk are not added
     double s = 0.0;
-    for (int c = 0; c < p.chunks; c++) s += a.partials[((size_t)e * p.chunks + c) * BA_NSUM + t];
+    const double* pe = a.partials + (size_t)e * p.chunks * BA_NSUM + t;
+    for (int c0 = 0; c0 < p.chunks; c0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = pe[(size_t)min(c0 + k, p.chunks - 1) * BA_NSUM];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (c0 + k < p.chunks) s += v[k];
+    }
     if (t < 28) {
       int r = 0, l = t;
       while (l >= 7 - r) {
