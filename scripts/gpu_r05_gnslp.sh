@@ -5,11 +5,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r05gs
 export TMPDIR=/tmp
-timeout -k 10 200 python3 -u scripts/track_dump.py gpurun_out/r05gs/new.npz > gpurun_out/r05gs/dump_new.txt 2>&1 || { tail -20 gpurun_out/r05gs/dump_new.txt; exit 1; }
-M3S_LIB=lightweight-mast3r-slam_amd/lib/ab/libm3s_noslp.so timeout -k 10 200 python3 -u scripts/track_dump.py gpurun_out/r05gs/noslp.npz > gpurun_out/r05gs/dump_noslp.txt 2>&1 || { tail -20 gpurun_out/r05gs/dump_noslp.txt; exit 1; }
+timeout -k 10 200 python3 -u scripts/track_dump.py /tmp/r05gs_new.npz > gpurun_out/r05gs/dump_new.txt 2>&1 || { tail -20 gpurun_out/r05gs/dump_new.txt; exit 1; }
+M3S_LIB=lightweight-mast3r-slam_amd/lib/ab/libm3s_noslp.so timeout -k 10 200 python3 -u scripts/track_dump.py /tmp/r05gs_noslp.npz > gpurun_out/r05gs/dump_noslp.txt 2>&1 || { tail -20 gpurun_out/r05gs/dump_noslp.txt; exit 1; }
 python3 - <<'PY'
 import numpy as np
-a, b = np.load("gpurun_out/r05gs/new.npz"), np.load("gpurun_out/r05gs/noslp.npz")
+a, b = np.load("/tmp/r05gs_new.npz"), np.load("/tmp/r05gs_noslp.npz")
 bad = [k for k in a.files if not np.array_equal(a[k], b[k])]
 print("bit-identical:", not bad, "arrays", len(a.files), "differing", bad[:10])
 PY
