@@ -141,6 +141,76 @@ __device__ __forceinline__ void setup_point(const TrackArgs& a, const TrackParam
   }
 }
 
+// setup_point (non-direct path) for K points of one thread at once, for the folded GN prologue: every point's own
+// loads first (idx, Qkf, Ck, the match flag, Xk), then every gather at idx (Qff, Cf, Xf), then the math, then the
+// byte-map stores, with no branch between the points: one point after another, each point's two dependent round
+// trips and the branches around them stacked up in front of the first iteration. A point at n >= N computes point
+// N - 1 again and counts, stores and marks nothing (its records are zero, as before). Same formulas as setup_point,
+// so the records and counts are the same bit for bit.
+template <int K>
+__device__ __forceinline__ void setup_points(const TrackArgs& a, const TrackParams& p, const int (&nn)[K],
+                                             float4 (&r0)[K], float4 (&r1)[K], int& v_opt, int& v_kf) {
+  int n[K];
+  bool act[K];
+  int64_t i[K];
+  float qkf[K], ck[K], xk[K][3];
+  bool vm[K];
+#pragma unroll
+  for (int u = 0; u < K; u++) {
+    act[u] = nn[u] < p.N;
+    n[u] = act[u] ? nn[u] : p.N - 1;
+    i[u] = a.idx[n[u]];
+    qkf[u] = a.Qkf[n[u]];
+    ck[u] = a.Ck[n[u]];
+    vm[u] = a.valid_match[n[u]] != 0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) xk[u][c] = a.Xk[(size_t)n[u] * 3 + c];
+  }
+  float qff[K], cf[K], xf[K][3];
+#pragma unroll
+  for (int u = 0; u < K; u++) {
+    qff[u] = a.Qff[i[u]];
+    cf[u] = a.Cf[i[u]];
+#pragma unroll
+    for (int c = 0; c < 3; c++) xf[u][c] = a.Xf[i[u] * 3 + c];
+  }
+#pragma unroll
+  for (int u = 0; u < K; u++) {
+    const float qk = sqrtf(qff[u] * qkf[u]);
+    const float cfa = cf[u] / p.Nf;  // frame.get_average_conf(): C / N
+    const float cka = ck[u] / p.Nk;
+    const bool valid_opt = vm[u] && (cfa > p.C_conf) && (cka > p.C_conf) && (qk > p.Q_conf);
+    v_opt += (act[u] && valid_opt) ? 1 : 0;
+    v_kf += (act[u] && vm[u] && (qk > p.Q_conf)) ? 1 : 0;
+    const float sq = valid_opt ? sqrtf(qk) : 0.0f;
+    float4 q0, q1;
+    if (p.mode == 0) {  // rays: [Xf[idx], rd_k = (Xk/|Xk|, |Xk|), sqrtQ*valid]
+      const float d = sqrtf(xk[u][0] * xk[u][0] + xk[u][1] * xk[u][1] + xk[u][2] * xk[u][2]);
+      const float di = 1.0f / d;
+      q0 = make_float4(xf[u][0], xf[u][1], xf[u][2], di * xk[u][0]);
+      q1 = make_float4(di * xk[u][1], di * xk[u][2], d, sq);
+    } else {  // calib: constrain_points_to_ray at pixel idx, meas_k = [u_n, v_n, log z_k]
+      const int i32 = (int)i[u], vi = i32 / p.W;  // 32-bit: i < H*W
+      const float uf = (float)(i32 - vi * p.W), vf = (float)vi;
+      const float zf = xf[u][2];
+      const float xc = zf * ((uf - p.cx) / p.fx);
+      const float yc = zf * ((vf - p.cy) / p.fy);
+      const float zk = xk[u][2];
+      const bool vmeas = zk > p.depth_eps;
+      const int vnn = n[u] / p.W;
+      const float un = (float)(n[u] - vnn * p.W), vn = (float)vnn;
+      q0 = make_float4(xc, yc, zf, vmeas ? un : 0.0f);
+      q1 = make_float4(vmeas ? vn : 0.0f, vmeas ? logf(zk) : 0.0f, vmeas ? 1.0f : 0.0f, sq);
+    }
+    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    r0[u] = act[u] ? q0 : z;
+    r1[u] = act[u] ? q1 : z;
+  }
+#pragma unroll
+  for (int u = 0; u < K; u++)
+    if (act[u] && vm[u]) a.flags[i[u]] = 1;  // benign same-value races; popcounted by the fuse launch
+}
+
 __global__ void __launch_bounds__(256) track_setup_kernel(TrackArgs a, TrackParams p) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n == 0) track_state_init(a.state, a.T_WCf, a.T_WCk);
@@ -654,21 +724,28 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
   const int n00 = blockIdx.x * GN_THREADS + threadIdx.x;
   float4 c0[GN_PPT], c1[GN_PPT];
   int v_opt = 0, v_kf = 0;  // SETUP: this thread's valid counts (iteration 0)
+  if (SETUP && !p.direct) {  // the first round's records built in one batch (setup_points)
+    int nn[GN_PPT];
 #pragma unroll
-  for (int u = 0; u < GN_PPT; u++) {
-    if constexpr (SETUP) {
-      const int n = n00 + u * stride;
-      c0[u] = c1[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (n < p.N) {
-        int vo = 0, vk = 0;
-        setup_point(a, p, n, c0[u], c1[u], vo, vk);
-        v_opt += vo;
-        v_kf += vk;
+    for (int u = 0; u < GN_PPT; u++) nn[u] = n00 + u * stride;
+    setup_points<GN_PPT>(a, p, nn, c0, c1, v_opt, v_kf);
+  } else {
+#pragma unroll
+    for (int u = 0; u < GN_PPT; u++) {
+      if constexpr (SETUP) {
+        const int n = n00 + u * stride;
+        c0[u] = c1[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (n < p.N) {
+          int vo = 0, vk = 0;
+          setup_point(a, p, n, c0[u], c1[u], vo, vk);
+          v_opt += vo;
+          v_kf += vk;
+        }
+      } else {
+        const int n = min(n00 + u * stride, p.N - 1);
+        c0[u] = rec[2 * (size_t)n];
+        c1[u] = rec[2 * (size_t)n + 1];
       }
-    } else {
-      const int n = min(n00 + u * stride, p.N - 1);
-      c0[u] = rec[2 * (size_t)n];
-      c1[u] = rec[2 * (size_t)n + 1];
     }
   }
   gu32* gran = (gu32*)(a.tick + M3S_TRACK_GRANULES);  // [2 parities][8 shards][72] x {half, tag}
