@@ -879,18 +879,28 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
     if (threadIdx.x < 64) {
       // wave 0 polls every shard's 72 granules (lane l: granules l, l + 64, ... of the nsh x 72), until every tag
       // is this iteration's
+      // (a poll round issues all of a lane's granule loads before it looks at any: one load, its wait and its tag
+      // test at a time made each round nine dependent round trips)
       const int ng = nsh * 2 * GN_NSUM;
+      constexpr int GPL = (M3S_TRACK_SHARDS * 2 * GN_NSUM + 63) / 64;  // granules per lane, at most
       unsigned spins = 0;
       for (;;) {
         bool ok = true;
-        for (int g = lane; g < ng; g += 64) {
-          const unsigned long long v = __hip_atomic_load(
-              (gull*)&gran[2 * (par * M3S_TRACK_SHARDS * 2 * GN_NSUM + g)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(v >> 32) != (unsigned)(it + 1)) {
-            ok = false;
-          } else {
-            unsigned* w = reinterpret_cast<unsigned*>(&s_shard[0][0]);
-            w[g] = (unsigned)v;  // lo/hi words in place: granule g = shard g / 72, sum (g % 72) / 2, half g % 2
+        unsigned long long gv[GPL];
+#pragma unroll
+        for (int k = 0; k < GPL; k++)
+          gv[k] = __hip_atomic_load((gull*)&gran[2 * (par * M3S_TRACK_SHARDS * 2 * GN_NSUM + min(lane + 64 * k, ng - 1))],
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < GPL; k++) {
+          const int g = lane + 64 * k;
+          if (g < ng) {
+            if ((unsigned)(gv[k] >> 32) != (unsigned)(it + 1)) {
+              ok = false;
+            } else {
+              unsigned* w = reinterpret_cast<unsigned*>(&s_shard[0][0]);
+              w[g] = (unsigned)gv[k];  // lo/hi words in place: granule g = shard g / 72, sum (g % 72) / 2, half g % 2
+            }
           }
         }
         if (__all(ok)) break;
@@ -920,10 +930,14 @@ __global__ void __launch_bounds__(GN_THREADS) gn_loop_kernel(TrackArgs a, TrackP
       // every block's counts were added before its iteration-0 ticket, and every shard sum seen above follows all
       // of its shard's tickets: the counters are complete (device-scope loads)
       if (threadIdx.x == 0) {
-        unsigned long long c = 0;
+        // the eight loads first, then the sum: written as c += load, the compiler kept each atomic load behind the
+        // previous one's wait (eight dependent round trips before the first solve)
+        unsigned long long cv[M3S_TRACK_SHARDS], c = 0;
 #pragma unroll
         for (int k = 0; k < M3S_TRACK_SHARDS; k++)
-          c += __hip_atomic_load(&a.cnt[16 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          cv[k] = __hip_atomic_load(&a.cnt[16 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < M3S_TRACK_SHARDS; k++) c += cv[k];
         s_cnt[0] = c;
       }
       __syncthreads();
