@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP-event spans inside the timed loop (no roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="test the N-rank launcher only (gloo, no GPU): rank 0 prints world size and a rank sum")
     return ap.parse_args()
 
 
@@ -246,10 +248,10 @@ def bench_store(args, dev, frames=60, warmup=10):
 def roofline(kern, N, gn_iters_mean):
     """Algorithmic bytes / flops per launch / measured HIP-event duration."""
     per_px_bytes = {
-        "prep_rays": 12 + 36,  # X11 in; rays9 out
-        # X21, idx_init, rays9, X11 gather, p1, valid; + the planar descriptor conversion riding along (D11 f32 in,
-        # D11 f16 out)
-        "proj_occlusion": 12 + 8 + 36 + 12 + 8 + 1 + 96 + 48,
+        # X11 in, rays9 out; + the D11 f32 -> f16 descriptor conversion, which runs in prep_rays (csrc/matching.hip
+        # prep_rays_kernel; DESIGN.md §4: 192 B/px)
+        "prep_rays": 12 + 36 + 96 + 48,
+        "proj_occlusion": 12 + 8 + 36 + 12 + 8 + 1,  # X21, idx_init, rays9, X11 gather, p1, valid (77 B/px)
         "refine_lin": 48 + 96 + 8 + 8,  # D11 f16 centre rows, D21 f32, p1, idx
         "track_setup": 8 + 1 + 12 + 4 + 4 + 12 + 4 + 4 + 32,  # idx, valid, Xf, Cf, Qff, Xk, Ck, Qkf -> rec
         "gn_iters": 32 * gn_iters_mean,  # 32 B record per point per iteration
@@ -682,11 +684,96 @@ def cpu_baseline(args):
                       + f"; one frame on one thread in {el1:.1f}s; value = the best thread count ({best})"}
 
 
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` with no launcher around it (WORLD_SIZE unset): start N rank processes of this
+    script, one per GPU (LOCAL_RANK = device), rendezvous on 127.0.0.1, and return the worst exit code. The parent
+    touches no GPU (torch.cuda.device_count() does not initialise HIP on this image); rank 0 prints the JSON line
+    to the inherited stdout. With M3S_BENCH_DEVICE set (the rehearsal of the N-rank path on one GPU, usually with
+    M3S_DIST_BACKEND=gloo) every rank runs on that device, so no device count is required."""
+    import signal
+    import subprocess
+
+    n = args.gpus
+    rehearsal = os.environ.get("M3S_BENCH_DEVICE") is not None or args.launch_probe
+    if not rehearsal:
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {have}; "
+                f"set M3S_BENCH_DEVICE=<dev> M3S_DIST_BACKEND=gloo to rehearse {n} ranks on one device")
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), M3S_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    log(f"bench.py: launched {n} ranks (pids {[p.pid for p in procs]}) on 127.0.0.1:{port}")
+    codes = [None] * n
+    try:
+        while any(c is None for c in codes):
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    codes[i] = p.poll()
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:  # one rank failed: its peers would wait for it at their next collective
+                for i, p in enumerate(procs):
+                    if codes[i] is None:
+                        p.send_signal(signal.SIGTERM)
+                for i, p in enumerate(procs):
+                    if codes[i] is None:
+                        try:
+                            codes[i] = p.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            codes[i] = p.wait()
+                break
+            time.sleep(0.2)
+    except BaseException:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise
+    worst = max((abs(c) for c in codes), default=0)
+    if worst:
+        log(f"bench.py: rank exit codes {codes}")
+    return worst
+
+
+def launch_probe(world, rank, args):
+    """--launch-probe: the launcher contract without a GPU (CPU test): every rank joins a gloo group, checks
+    world == --gpus, all-reduces its rank, and rank 0 prints one JSON line."""
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "rank_sum": float(t.item()),
+                          "launcher": os.environ.get("M3S_BENCH_LAUNCHER", "external")}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: rank {rank} sees WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU "
+            f"(torch.distributed.run --nproc-per-node {args.gpus}, or plain `python bench.py --gpus {args.gpus}`)")
+        sys.exit(2)
+    if args.launch_probe:
+        launch_probe(world, rank, args)
+        return
     # M3S_BENCH_DEVICE / M3S_DIST_BACKEND: rehearsal of the N-rank path on a 1-GPU box (all ranks on
     # one device over gloo); the driver's multi-GPU runs use one GPU per rank over RCCL ("nccl").
     ndev = os.environ.get("M3S_BENCH_DEVICE")
@@ -744,6 +831,11 @@ def main():
                                    f"({'calib' if args.mode == 'calib' else 'rays'} mode), {args.height}x"
                                    f"{args.width} pointmap pairs, GN to convergence",
                        "parallelism": f"replicas x{world} (tracking does not shard)",
+                       "launch": {"world_size": world, "gpus_arg": args.gpus,
+                                  "launcher": os.environ.get("M3S_BENCH_LAUNCHER", "torch.distributed.run"
+                                                             if "TORCHELASTIC_RUN_ID" in os.environ else
+                                                             ("external" if world > 1 else "none")),
+                                  "backend": dist.get_backend() if world > 1 else None},
                        "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
             "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,

@@ -145,6 +145,8 @@ int m3s_ba_reuse_release(const void* workspace);
  * m3s_ba_plan_release(workspace) once no plan on `workspace` will be solved again and before freeing or repurposing
  * it (m3s_ba_reuse_release does it too); it joins a pending analysis and frees its tables. */
 int m3s_ba_plan_release(const void* workspace);
+/* Diagnostic: how many workspaces currently hold BA plan state (a leak check for callers that cache workspaces). */
+int m3s_ba_plan_count(void);
 int m3s_ba_edge_sums(const m3s_ba_plan* plan, size_t* byte_offset, size_t* byte_count);
 int m3s_ba_linearize(const m3s_ba_plan* plan, void* stream);
 int m3s_ba_solve(const m3s_ba_plan* plan, void* stream);

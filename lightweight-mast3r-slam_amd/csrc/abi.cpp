@@ -1467,6 +1467,11 @@ extern "C" int m3s_ba_plan_release(const void* workspace) {
   return M3S_OK;
 }
 
+extern "C" int m3s_ba_plan_count(void) {
+  std::lock_guard<std::mutex> lock(g_sym_mu);
+  return (int)g_sym.size();
+}
+
 extern "C" int m3s_ba_reuse_release(const void* workspace) {
   m3s_ba_plan_release(workspace);
   std::lock_guard<std::mutex> lock(g_rec_mu);

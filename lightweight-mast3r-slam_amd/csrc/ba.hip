@@ -25,6 +25,7 @@
 #include "m3s_common.hpp"
 #include "m3s_ba.h"
 #include "ba_pattern.h"  // BA_BS_* flags of the dataflow back-substitution lists
+#include <cstring>
 
 namespace m3s {
 
@@ -235,8 +236,12 @@ __device__ __forceinline__ void rec_store(float4* slot, int k, float4 r) {
   // records: streamed out once per call (non-temporal under BA_PACK_NT, like the pack's input streams)
 #if BA_PACK_NT
   if constexpr (MODE == BA_MODE_CALIB) {
-    typedef float f3v __attribute__((ext_vector_type(3)));
-    __builtin_nontemporal_store(f3v{r.x, r.y, r.z}, reinterpret_cast<f3v*>(reinterpret_cast<float*>(slot) + 3 * (size_t)k));
+    // three 4-B stores, 12 B by construction: a vec3 store may legally be widened to 16 B, which would overwrite the
+    // next record's first word (the backend merges these into one dwordx3)
+    float* d = reinterpret_cast<float*>(slot) + 3 * (size_t)k;
+    __builtin_nontemporal_store(r.x, d);
+    __builtin_nontemporal_store(r.y, d + 1);
+    __builtin_nontemporal_store(r.z, d + 2);
   } else {
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{r.x, r.y, r.z, r.w}, reinterpret_cast<f4v*>(slot + k));
@@ -1870,10 +1875,20 @@ extern "C" hipError_t m3s_launch_ba_snode(const BaArgs* a, int nwg, hipStream_t 
 // XCD affinity of the solve (M3S_BA_XCD0, default on): every multi-workgroup factor step and the one-workgroup kernel
 // (block 0) run on XCD 0, so each step reads the previous one's blocks from that XCD's L2 instead of across the
 // fabric. Measured (scripts/gpu_r05_xcd.sh, same box, two pairs): solve C5 0.393 -> 0.375 ms, C4 0.424 -> 0.409 ms.
+// The stride assumes the round-robin workgroup dispatch over 8 XCDs of an MI3xx part in SPX mode (one device = the
+// whole package): it is used only when the device is a gfx94x / gfx950 that reports at least 8 x 32 CUs. A partition
+// (CPX: one XCD per device, 32 CUs) or any other part gets stride 1, where the 7 of 8 idle blocks would be wasted
+// dispatches and the L2 locality would not exist.
 static int ba_xcd_stride() {
   static const int xs = [] {
     const char* e = getenv("M3S_BA_XCD0");
-    return (e && atoi(e) == 0) ? 1 : 8;
+    if (e && atoi(e) == 0) return 1;
+    int dev = 0, cus = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1;
+    cus = prop.multiProcessorCount;
+    const bool mi3xx = strncmp(prop.gcnArchName, "gfx94", 5) == 0 || strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    return (mi3xx && cus >= 8 * 32 && cus % 8 == 0) ? 8 : 1;
   }();
   return xs;
 }

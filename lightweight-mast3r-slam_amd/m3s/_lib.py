@@ -95,6 +95,7 @@ _SIGS = {
     "m3s_ba_reuse_info": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_int), ctypes.POINTER(c_int)], c_int),
     "m3s_ba_reuse_release": ([c_void_p], c_int),
     "m3s_ba_plan_release": ([c_void_p], c_int),
+    "m3s_ba_plan_count": ([], c_int),
     "m3s_ba_edge_sums": ([ctypes.POINTER(BaPlan), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)], c_int),
     "m3s_ba_linearize": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
     "m3s_ba_solve": ([ctypes.POINTER(BaPlan), c_void_p], c_int),
@@ -181,9 +182,11 @@ def ptr(t):
 _WS = {}
 
 
-# key -> the ABI call that forgets a dropped buffer (BA workspaces are not cached here: HipShard / RecordCache own and
-# release theirs)
-_WS_RELEASE = {"track": "m3s_track_release"}
+# key -> the ABI call that forgets a dropped buffer's per-workspace library state: the tracker's clean-scratch record,
+# and the BA plan state of the workspace mast3r_slam_backends' gauss_newton_* cache under "ba" (it grows with E, so a
+# growing SLAM run replaces it at nearly every backend solve; without the release every dropped buffer's PlanSym
+# would stay in the library's table). HipShard / RecordCache own and release their own workspaces.
+_WS_RELEASE = {"track": "m3s_track_release", "ba": "m3s_ba_plan_release"}
 
 
 def workspace(key, nbytes, device, stream):

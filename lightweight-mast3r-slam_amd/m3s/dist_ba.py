@@ -161,15 +161,27 @@ class HipShard:
         _lib.check(self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev)))
         return it.value
 
-    def stalled(self):
-        """True when this rank's factor schedule stalled (M3S_ESTALL: its GN loop stopped); any other error
-        raises. One readback (syncs the stream)."""
+    def status(self):
+        """This rank's loop status code, without raising: 0, M3S_ESTALL (its factor schedule stalled and its GN
+        loop stopped) or another m3s error code. One readback (syncs the stream)."""
         it = ctypes.c_int()
-        rc = self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev))
+        return int(self.lib.m3s_ba_iterations(ctypes.byref(self.plan), ctypes.byref(it), _lib.stream_ptr(self.dev)))
+
+    def stalled(self):
+        """True when this rank's factor schedule stalled; any other error raises."""
+        rc = self.status()
         if rc == M3S_ESTALL:
             return True
         _lib.check(rc)
         return False
+
+
+def _shard_status(shard):
+    if hasattr(shard, "status"):
+        return int(shard.status())
+    if hasattr(shard, "stalled"):
+        return M3S_ESTALL if shard.stalled() else 0
+    return 0
 
 
 def run_sharded(shard, max_iter, group=None):
@@ -183,16 +195,21 @@ def run_sharded(shard, max_iter, group=None):
         if reduce:
             dist.all_reduce(shard.edge_sums, op=dist.ReduceOp.SUM, group=group)
         shard.solve()
-    # The stall decision is global: a rank whose bounded factor-schedule wait timed out stops its own loop (its
-    # edge-sum rows stay zero), so its peers solved without that shard. One MAX all-reduce of the flag after the loop
-    # makes every rank raise together, instead of the stalled rank alone (whose peers would then wait for it at their
-    # next collective).
-    stalled = bool(shard.stalled()) if hasattr(shard, "stalled") else False
+    # The outcome is decided globally: a rank whose bounded factor-schedule wait timed out stops its own loop (its
+    # edge-sum rows stay zero), so its peers solved without that shard, and a rank whose status readback failed
+    # otherwise must not raise alone either (its peers would wait for it at their next collective). Every rank reads
+    # its status code without raising, one MAX all-reduce of {stalled, failed, |code|} follows, and then every rank
+    # raises the same error together.
+    rc = _shard_status(shard)
+    stalled, failed, code = float(rc == M3S_ESTALL), float(rc != 0 and rc != M3S_ESTALL), float(abs(rc))
     if reduce:
-        flag = torch.tensor([1.0 if stalled else 0.0], dtype=torch.float64, device=shard.edge_sums.device)
+        flag = torch.tensor([stalled, failed, code if failed else 0.0], dtype=torch.float64,
+                            device=shard.edge_sums.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        stalled = bool(flag.item() > 0.0)
-    if stalled:
+        stalled, failed, code = (float(v) for v in flag.tolist())
+    if failed > 0.0:
+        raise RuntimeError(f"m3s error {-int(code)}: ba: the GN loop failed on a rank; the poses are not valid")
+    if stalled > 0.0:
         raise RuntimeError(f"m3s error {M3S_ESTALL}: ba: a factor-schedule hand-off stalled on a rank (bounded wait "
                            "timed out); the GN loop stopped and the poses are not valid")
     return shard

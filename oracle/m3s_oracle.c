@@ -129,9 +129,15 @@ static inline void m3o_bilinear_weights(float u, float v, int* u11, int* v11, fl
   w[3] = (float)((1.0 - (double)du) * (1.0 - (double)dv)); /* w22 */
 }
 
-void m3o_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
-                   uint8_t* converged, int B, int H, int W, int N, int max_iter, float lambda_init,
-                   float cost_thresh) {
+/* diag (optional, test infrastructure for the fused match's mismatch census): per pixel
+ *   [0] the smallest LM accept margin over the iterations, |new_cost - cost| / (sqrt(cost) + sqrt(new_cost)): a
+ *       rounding-level difference in either cost (each is a sum of squares of err = r - p, err's rounding ~ ulp(|r|))
+ *       can flip the accept / reject branch only when this is of the order of that rounding;
+ *   [1] the last iteration's convergence margin, |c - cost_thresh| / (sqrt(c) + sqrt(cost_thresh)) for the cost c the
+ *       converged flag was decided on. */
+static void iter_proj_impl(const float* rays, const float* pts, const float* p_init, float* p_new,
+                           uint8_t* converged, int B, int H, int W, int N, int max_iter, float lambda_init,
+                           float cost_thresh, float* diag) {
 #pragma omp parallel for collapse(2) schedule(static)
   for (int b = 0; b < B; b++) {
     for (int n = 0; n < N; n++) {
@@ -143,6 +149,7 @@ void m3o_iter_proj(const float* rays, const float* pts, const float* p_init, flo
       m3o_clamp(&v, 1.0f, (float)(H - 2));
       uint8_t conv = 0;
       float lambda = lambda_init;
+      double acc_margin = INFINITY, conv_margin = INFINITY;
       for (int it = 0; it < max_iter; it++) {
         int u11, v11;
         float w[4];
@@ -185,6 +192,12 @@ void m3o_iter_proj(const float* rays, const float* pts, const float* p_init, flo
         for (int j = 0; j < 3; j++) r[j] *= r_norm_inv;
         for (int j = 0; j < 3; j++) err[j] = r[j] - p[j];
         float new_cost = err[0] * err[0] + err[1] * err[1] + err[2] * err[2];
+        /* a step that rounds to no move (u_new == u, v_new == v) compares a cost with itself: no rounding can flip it */
+        if (diag && (u_new != u || v_new != v)) {
+          const double m = fabs((double)new_cost - (double)cost) / (sqrt((double)cost) + sqrt((double)new_cost) + 1e-30);
+          if (m < acc_margin) acc_margin = m;
+        }
+        const float decided = new_cost < cost ? new_cost : cost;
         if (new_cost < cost) {
           u = u_new;
           v = v_new;
@@ -194,12 +207,31 @@ void m3o_iter_proj(const float* rays, const float* pts, const float* p_init, flo
           lambda = (float)((double)lambda * 10.0);
           conv = cost < cost_thresh;
         }
+        if (diag)
+          conv_margin = fabs((double)decided - (double)cost_thresh) /
+                        (sqrt((double)decided) + sqrt((double)cost_thresh) + 1e-30);
       }
       p_new[((size_t)b * N + n) * 2 + 0] = u;
       p_new[((size_t)b * N + n) * 2 + 1] = v;
       converged[(size_t)b * N + n] = conv;
+      if (diag) {
+        diag[((size_t)b * N + n) * 2 + 0] = (float)acc_margin;
+        diag[((size_t)b * N + n) * 2 + 1] = (float)conv_margin;
+      }
     }
   }
+}
+
+void m3o_iter_proj(const float* rays, const float* pts, const float* p_init, float* p_new,
+                   uint8_t* converged, int B, int H, int W, int N, int max_iter, float lambda_init,
+                   float cost_thresh) {
+  iter_proj_impl(rays, pts, p_init, p_new, converged, B, H, W, N, max_iter, lambda_init, cost_thresh, NULL);
+}
+
+void m3o_iter_proj_diag(const float* rays, const float* pts, const float* p_init, float* p_new,
+                        uint8_t* converged, int B, int H, int W, int N, int max_iter, float lambda_init,
+                        float cost_thresh, float* diag) {
+  iter_proj_impl(rays, pts, p_init, p_new, converged, B, H, W, N, max_iter, lambda_init, cost_thresh, diag);
 }
 
 /* ------------------------------------------------------------------------------------------ */

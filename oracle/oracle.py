@@ -61,6 +61,8 @@ def lib():
             subprocess.check_call(["make", "-C", _HERE, "-s"])
         L = ctypes.CDLL(path)
         L.m3o_iter_proj.argtypes = [_f32p, _f32p, _f32p, _f32p, _u8p] + [ctypes.c_int] * 5 + [ctypes.c_float] * 2
+        L.m3o_iter_proj_diag.argtypes = ([_f32p, _f32p, _f32p, _f32p, _u8p] + [ctypes.c_int] * 5 + [ctypes.c_float] * 2
+                                         + [_f32p])
         L.m3o_refine_matches_f16.argtypes = [_u16p, _u16p, _i64p, _i64p] + [ctypes.c_int] * 7
         L.m3o_refine_matches_f32.argtypes = [_f32p, _f32p, _i64p, _i64p] + [ctypes.c_int] * 7
         L.m3o_f32_to_f16.argtypes = [_f32p, _u16p, ctypes.c_int64]
@@ -103,6 +105,21 @@ def iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh):
     lib().m3o_iter_proj(_p(rays, _f32p), _p(pts, _f32p), _p(p_init, _f32p), _p(p_new, _f32p), _p(conv, _u8p),
                         B, H, W, N, int(max_iter), float(lambda_init), float(cost_thresh))
     return p_new, conv.astype(bool)
+
+
+def iter_proj_diag(rays, pts, p_init, max_iter, lambda_init, cost_thresh):
+    """iter_proj + per-pixel rounding margins (m3s_oracle.c iter_proj_impl): (p_new, converged, diag (B,N,2)) with
+    diag[..., 0] the smallest LM accept margin and diag[..., 1] the convergence-threshold margin."""
+    rays, pts, p_init = _c(rays, np.float32), _c(pts, np.float32), _c(p_init, np.float32)
+    B, H, W, C = rays.shape
+    assert C == 9
+    N = pts.shape[1]
+    p_new = np.zeros((B, N, 2), np.float32)
+    conv = np.zeros((B, N), np.uint8)
+    diag = np.zeros((B, N, 2), np.float32)
+    lib().m3o_iter_proj_diag(_p(rays, _f32p), _p(pts, _f32p), _p(p_init, _f32p), _p(p_new, _f32p), _p(conv, _u8p),
+                             B, H, W, N, int(max_iter), float(lambda_init), float(cost_thresh), _p(diag, _f32p))
+    return p_new, conv.astype(bool), diag
 
 
 def to_half_bits(x):
@@ -283,6 +300,23 @@ def match(X11, X21, D11, D21, idx_init=None, max_iter=10, lambda_init=1e-8, conv
     if radius > 0:
         p1 = refine_matches(D11, D21.reshape(b, h * w, -1), p1, radius, dilation_max)
     return pixel_to_lin(p1, w), valid[..., None]
+
+
+def match_diag(X11, X21, D11, D21, idx_init=None, max_iter=10, lambda_init=1e-8, convergence_thresh=1e-6,
+               dist_thresh=0.1, radius=3, dilation_max=5):
+    """``match`` with its intermediates, for the fused match's mismatch census (tests/test_gpu_configs.py): a dict
+    of idx, valid (the outputs of ``match``), p_new (B,N,2) float, p1 (B,N) linear truncated index before the refine,
+    conv, the occlusion distance d (B,N) and the LM margins of ``iter_proj_diag``."""
+    b, h, w = X21.shape[:3]
+    rays, pts, p_init = prep_for_iter_proj(X11, X21, idx_init)
+    p_new, conv, diag = iter_proj_diag(rays, pts, p_init, max_iter, lambda_init, convergence_thresh)
+    p1 = p_new.astype(np.int64)
+    Xg = X11[np.arange(b)[:, None], p1[..., 1], p1[..., 0], :].reshape(b, h, w, 3)
+    d = np.sqrt(((Xg.astype(np.float64) - X21) ** 2).sum(-1)).reshape(b, -1)
+    valid = conv & (d < dist_thresh)
+    p1r = refine_matches(D11, D21.reshape(b, h * w, -1), p1, radius, dilation_max) if radius > 0 else p1
+    return {"idx": pixel_to_lin(p1r, w), "valid": valid[..., None], "p_new": p_new, "p1": pixel_to_lin(p1, w),
+            "conv": conv, "d": d, "accept_margin": diag[..., 0], "conv_margin": diag[..., 1]}
 
 
 # ---- Sim3 fp64 (lietorch semantics) ----

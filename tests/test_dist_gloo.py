@@ -161,6 +161,43 @@ def _stall_main(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+class _ErrorShard(_StallShard):
+    """A shard whose status readback failed on rank 1 with a non-stall error (it must not raise
+    before the collective)."""
+
+    def status(self):
+        return -2 if self.rank == 1 else 0
+
+
+def _error_main(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from m3s.dist_ba import run_sharded
+
+        try:
+            run_sharded(_ErrorShard(rank), 2)
+            msg = "no error"
+        except RuntimeError as e:
+            msg = str(e)
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        with open(os.path.join(out_dir, f"err_r{rank}.txt"), "w") as f:
+            f.write(f"{msg}|{t.item()}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_sharded_ba_error_raises_on_every_rank(tmp_path):
+    mp.spawn(_error_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        msg, tot = open(os.path.join(tmp_path, f"err_r{r}.txt")).read().split("|")
+        assert "m3s error -2" in msg, f"rank {r}: {msg}"
+        assert float(tot) == 2.0
+
+
 @pytest.mark.timeout(120)
 def test_sharded_ba_stall_raises_on_every_rank(tmp_path):
     """a stall on one rank (its loop stopped, its edge-sum rows zero) is a global decision: one MAX

@@ -163,6 +163,27 @@ def test_ba_converges_to_ground_truth_on_consistent_graph():
         np.testing.assert_allclose(T, Twc_gt, atol=2e-6)
 
 
+def test_growing_backend_workspace_releases_plan_state():
+    """mast3r_slam_backends caches its BA workspace under "ba" and regrows it as E grows; each
+    dropped buffer's library plan state must be released with it (m3s_ba_plan_release), or the host table image of
+    every replaced workspace stays in the library for good. Replays a growing graph and watches the plan count."""
+    from m3s import _lib
+
+    from m3s.synthetic import make_graph, two_way
+
+    lib = _lib.load()
+    G = make_graph(n_kf=12, H=8, W=12, seed=4)
+    ii, jj, idx, valid, Q = (t.numpy() for t in two_way(G))
+    counts = []
+    for n_kf in range(3, 13):  # every solve adds a keyframe and its edges: the workspace regrows
+        e = np.flatnonzero((ii < n_kf) & (jj < n_kf))
+        _call("rays", G["Twc0"].numpy()[:n_kf], G["Xs"].numpy()[:n_kf], G["Cs"].numpy()[:n_kf], ii[e], jj[e], idx[e],
+              valid[e], Q[e], None, 0, 0, max_iter=2)
+        counts.append(lib.m3s_ba_plan_count())
+    torch.cuda.synchronize()
+    assert max(counts) - min(counts) <= 1, f"BA plan state grows with the replaced workspaces: {counts}"
+
+
 def test_singular_system_returns_zero_step():
     """No valid matches -> H singular -> LLT fails -> dx = 0 and Twc unchanged (gn_kernels.cu:147-150)."""
     N = 256
