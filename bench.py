@@ -35,6 +35,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 matrix-core peak (no sparsit
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector spec
 
 
+OUT = sys.stdout  # the JSON line's stream (main() points it at the original stdout)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -755,7 +758,7 @@ def launch_probe(world, rank, args):
     dist.all_reduce(t)
     if rank == 0:
         print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "rank_sum": float(t.item()),
-                          "launcher": os.environ.get("M3S_BENCH_LAUNCHER", "external")}), flush=True)
+                          "launcher": os.environ.get("M3S_BENCH_LAUNCHER", "external")}), file=OUT, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -771,6 +774,11 @@ def main():
         log(f"bench.py: rank {rank} sees WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU "
             f"(torch.distributed.run --nproc-per-node {args.gpus}, or plain `python bench.py --gpus {args.gpus}`)")
         sys.exit(2)
+    # stdout carries exactly one line, the JSON record: anything else a library prints there (gloo's "[Gloo] Rank ...
+    # is connected" lines, RCCL banners) goes to stderr
+    global OUT
+    OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.launch_probe:
         launch_probe(world, rank, args)
         return
@@ -841,7 +849,7 @@ def main():
             "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,
             "retrieval": retrieval, "store": store, "configs": configs,
         }
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec), file=OUT, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -53,6 +53,12 @@ __device__ __forceinline__ float desc_planar(const float4 v[6], h1* __restrict__
 // pixel per thread) with the tile's descriptor-norm partial max |D11h[pixel]|_2 into cnorm_part (nullable), else in
 // the (B,H,W,F) layout of the per-pixel refine kernels.
 // ------------------------------------------------------------------------------------------
+// torch.linalg.vector_norm / F.normalize of an fp32 3-vector in the reference's rounding: sqrt(fma(z, z, fma(y, y,
+// x * x))) (pinned bit for bit against the reference run's golden rays / pts; oracle m3o_norm3)
+__device__ __forceinline__ float norm3_ref(float x, float y, float z) {
+  return sqrtf(__builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
+}
+
 #define PREP_T 16
 // DMODE: 0 no descriptors, 1 planar (refine tile path), 2 the (B,H,W,F) row layout; a template argument so the
 // planar path's descriptor loads, issued first, cross no branch join (a runtime `if` made the compiler convert them,
@@ -96,7 +102,7 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
     const int t = threadIdx.x + 256 * r;
     if (t < HALO) {
       const float a = hv[r][0], c = hv[r][1], d = hv[r][2];
-      const float n = fmaxf(sqrtf(a * a + c * c + d * d), 1e-12f);
+      const float n = fmaxf(norm3_ref(a, c, d), 1e-12f);
       tile[t * 3 + 0] = a / n;
       tile[t * 3 + 1] = c / n;
       tile[t * 3 + 2] = d / n;
@@ -109,11 +115,29 @@ __global__ void __launch_bounds__(256) prep_rays_kernel(const float* __restrict_
 #pragma unroll
     for (int c = 0; c < 3; c++) {
       o[c] = T3(0, 0, c);
-      // gx kernel (1/32)[[-3,0,3],[-10,0,10],[-3,0,3]]; gy its transpose (image.py:10-24)
-      const float gx = -0.09375f * T3(-1, -1, c) + 0.09375f * T3(-1, 1, c) - 0.3125f * T3(0, -1, c) +
-                       0.3125f * T3(0, 1, c) - 0.09375f * T3(1, -1, c) + 0.09375f * T3(1, 1, c);
-      const float gy = -0.09375f * T3(-1, -1, c) - 0.3125f * T3(-1, 0, c) - 0.09375f * T3(-1, 1, c) +
-                       0.09375f * T3(1, -1, c) + 0.3125f * T3(1, 0, c) + 0.09375f * T3(1, 1, c);
+      // gx kernel (1/32)[[-3,0,3],[-10,0,10],[-3,0,3]]; gy its transpose (image.py:10-24), in the reference's
+      // depthwise conv2d order: a row-major FMA chain over all 9 taps, zero taps included (bit-exact against the
+      // reference run's rays: tests/golden/matching_48x64.npz, oracle m3o_img_gradient)
+      const float t00 = T3(-1, -1, c), t01 = T3(-1, 0, c), t02 = T3(-1, 1, c), t10 = T3(0, -1, c), t11 = T3(0, 0, c),
+                  t12 = T3(0, 1, c), t20 = T3(1, -1, c), t21 = T3(1, 0, c), t22 = T3(1, 1, c);
+      float gx = -0.09375f * t00;
+      gx = __builtin_fmaf(0.0f, t01, gx);
+      gx = __builtin_fmaf(0.09375f, t02, gx);
+      gx = __builtin_fmaf(-0.3125f, t10, gx);
+      gx = __builtin_fmaf(0.0f, t11, gx);
+      gx = __builtin_fmaf(0.3125f, t12, gx);
+      gx = __builtin_fmaf(-0.09375f, t20, gx);
+      gx = __builtin_fmaf(0.0f, t21, gx);
+      gx = __builtin_fmaf(0.09375f, t22, gx);
+      float gy = -0.09375f * t00;
+      gy = __builtin_fmaf(-0.3125f, t01, gy);
+      gy = __builtin_fmaf(-0.09375f, t02, gy);
+      gy = __builtin_fmaf(0.0f, t10, gy);
+      gy = __builtin_fmaf(0.0f, t11, gy);
+      gy = __builtin_fmaf(0.0f, t12, gy);
+      gy = __builtin_fmaf(0.09375f, t20, gy);
+      gy = __builtin_fmaf(0.3125f, t21, gy);
+      gy = __builtin_fmaf(0.09375f, t22, gy);
       o[3 + c] = gx;
       o[6 + c] = gy;
     }
@@ -386,7 +410,7 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
   if (n >= N) return;
   const size_t bn = (size_t)b * N + n;
   const float x = X21[bn * 3 + 0], y = X21[bn * 3 + 1], z = X21[bn * 3 + 2];
-  const float nrm = fmaxf(sqrtf(x * x + y * y + z * z), 1e-12f);
+  const float nrm = fmaxf(norm3_ref(x, y, z), 1e-12f);  // F.normalize (matching.py:44)
   const float p[3] = {x / nrm, y / nrm, z / nrm};
   float u, v;
   lin_to_pixel_f(idx_init != nullptr ? idx_init[bn] : (int64_t)n, W, u, v);
@@ -396,7 +420,7 @@ __global__ void __launch_bounds__(256) proj_occlusion_kernel(
                         X11 + (size_t)b * H * W * 3, Xg);
   const int pu = (int)u, pv = (int)v;  // .long() truncation; u,v >= 1 after clamping
   const float dx = Xg[0] - x, dy = Xg[1] - y, dz = Xg[2] - z;
-  const float d = sqrtf(dx * dx + dy * dy + dz * dz);
+  const float d = norm3_ref(dx, dy, dz);  // torch.linalg.norm (matching.py:71-73)
   p1[bn * 2 + 0] = pu;
   p1[bn * 2 + 1] = pv;
   valid[bn] = conv && (d < dist_thresh);

@@ -129,6 +129,62 @@ static inline void m3o_bilinear_weights(float u, float v, int* u11, int* v11, fl
   w[3] = (float)((1.0 - (double)du) * (1.0 - (double)dv)); /* w22 */
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* prep_for_iter_proj's torch glue (matching.py:25-49, image.py:5-38) in the reference's own fp32 */
+/* arithmetic. Pinned against the reference run (tests/golden/matching_48x64.npz rays / pts, bit  */
+/* for bit; tests/test_oracle.py): torch's CPU vector_norm of a 3-vector is the FMA chain          */
+/* sqrt(fma(z, z, fma(y, y, x * x))), F.normalize divides by max(norm, eps), and the depthwise     */
+/* conv2d of the reflect-padded image is a row-major FMA chain over all 9 taps, zero taps included */
+/* (acc = w00 * v00, then acc = fma(w, v, acc)).                                                   */
+/* ------------------------------------------------------------------------------------------ */
+static inline float m3o_norm3f(float x, float y, float z) { return sqrtf(fmaf(z, z, fmaf(y, y, x * x))); }
+
+void m3o_norm3(const float* x, float* out, int64_t n) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; i++) out[i] = m3o_norm3f(x[3 * i], x[3 * i + 1], x[3 * i + 2]);
+}
+
+void m3o_normalize3(const float* x, float* out, int64_t n) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; i++) {
+    const float nr = fmaxf(m3o_norm3f(x[3 * i], x[3 * i + 1], x[3 * i + 2]), 1e-12f);
+    for (int c = 0; c < 3; c++) out[3 * i + c] = x[3 * i + c] / nr;
+  }
+}
+
+/* img (B,H,W,3) -> gx, gy (B,H,W,3); F.pad(mode="reflect") by 1, kernel (1/32) [[-3,0,3],[-10,0,10],[-3,0,3]] and
+ * its transpose (image.py:10-24: the weights are (1/32) * integer, exact in fp32) */
+void m3o_img_gradient(const float* img, float* gx, float* gy, int B, int H, int W) {
+  static const float kx[3][3] = {{-0.09375f, 0.0f, 0.09375f}, {-0.3125f, 0.0f, 0.3125f}, {-0.09375f, 0.0f, 0.09375f}};
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int b = 0; b < B; b++) {
+    for (int y = 0; y < H; y++) {
+      for (int x = 0; x < W; x++) {
+        for (int c = 0; c < 3; c++) {
+          float ax = 0.0f, ay = 0.0f;
+          for (int t = 0; t < 9; t++) {
+            const int dy = t / 3 - 1, dx = t % 3 - 1;
+            int yy = y + dy, xx = x + dx;
+            yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+            xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+            const float v = img[(((size_t)b * H + yy) * W + xx) * 3 + c];
+            const float wx = kx[t / 3][t % 3], wy = kx[t % 3][t / 3];
+            if (t == 0) {
+              ax = wx * v;
+              ay = wy * v;
+            } else {
+              ax = fmaf(wx, v, ax);
+              ay = fmaf(wy, v, ay);
+            }
+          }
+          gx[(((size_t)b * H + y) * W + x) * 3 + c] = ax;
+          gy[(((size_t)b * H + y) * W + x) * 3 + c] = ay;
+        }
+      }
+    }
+  }
+}
+
 /* diag (optional, test infrastructure for the fused match's mismatch census): per pixel
  *   [0] the smallest LM accept margin over the iterations, |new_cost - cost| / (sqrt(cost) + sqrt(new_cost)): a
  *       rounding-level difference in either cost (each is a sum of squares of err = r - p, err's rounding ~ ulp(|r|))

@@ -75,6 +75,9 @@ def lib():
                                        _i64p, _i64p, _i64p, _u8p, _f32p, _f32p, _f64p, _f64p]
         L.m3o_pose_retr.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_int]
         L.m3o_exp_sim3.argtypes = [_f32p, _f32p]
+        L.m3o_norm3.argtypes = [_f32p, _f32p, ctypes.c_int64]
+        L.m3o_normalize3.argtypes = [_f32p, _f32p, ctypes.c_int64]
+        L.m3o_img_gradient.argtypes = [_f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.m3o_set_threads.argtypes = [ctypes.c_int]
         L.m3o_set_ref_order.argtypes = [ctypes.c_int]
         L.m3o_act_sim3.argtypes = [_f32p, _f32p, _f32p]
@@ -245,25 +248,33 @@ def exp_sim3_f32(xi):
 # --------------------------------------------------------------------------------------------
 # glue (numpy restatement)
 # --------------------------------------------------------------------------------------------
+def norm3(x):
+    """torch.linalg.vector_norm(x, dim=-1) of fp32 3-vectors on torch's CPU: sqrt(fma(z, z, fma(y, y, x * x))) in fp32
+    (m3s_oracle.c m3o_norm3; bit-exact against the reference run's golden vectors)."""
+    x = _c(x, np.float32)
+    out = np.empty(x.shape[:-1], np.float32)
+    lib().m3o_norm3(_p(x, _f32p), _p(out, _f32p), out.size)
+    return out
+
+
 def normalize(x, eps=1e-12):
-    """torch.nn.functional.normalize(x, dim=-1)."""
-    n = np.sqrt((x.astype(np.float64) ** 2).sum(-1, keepdims=True))
-    return (x / np.maximum(n, eps)).astype(x.dtype)
+    """torch.nn.functional.normalize(x, dim=-1) of fp32 3-vectors: x / max(norm3(x), eps) in fp32."""
+    assert eps == 1e-12
+    x = _c(x, np.float32)
+    out = np.empty_like(x)
+    lib().m3o_normalize3(_p(x, _f32p), _p(out, _f32p), x.size // 3)
+    return out
 
 
 def img_gradient(img):
-    """image.py:5-38 on (B,H,W,C): Scharr-like 3x3 / 32, reflect pad 1, depthwise."""
-    p = np.pad(img, ((0, 0), (1, 1), (1, 1), (0, 0)), mode="reflect").astype(np.float64)
-    k = np.array([[-3.0, 0.0, 3.0], [-10.0, 0.0, 10.0], [-3.0, 0.0, 3.0]]) / 32.0
-    H, W = img.shape[1:3]
-    gx = np.zeros(img.shape, np.float64)
-    gy = np.zeros(img.shape, np.float64)
-    for dy in range(3):
-        for dx in range(3):
-            win = p[:, dy:dy + H, dx:dx + W, :]
-            gx += k[dy, dx] * win
-            gy += k.T[dy, dx] * win
-    return gx.astype(np.float32), gy.astype(np.float32)
+    """image.py:5-38 on (B,H,W,3): Scharr-like 3x3 / 32, reflect pad 1, depthwise, in the reference's fp32 order
+    (m3s_oracle.c m3o_img_gradient: row-major FMA chain over the 9 taps)."""
+    img = _c(img, np.float32)
+    B, H, W, C = img.shape
+    assert C == 3
+    gx, gy = np.empty_like(img), np.empty_like(img)
+    lib().m3o_img_gradient(_p(img, _f32p), _p(gx, _f32p), _p(gy, _f32p), B, H, W)
+    return gx, gy
 
 
 def lin_to_pixel(idx, w):
@@ -295,8 +306,8 @@ def match(X11, X21, D11, D21, idx_init=None, max_iter=10, lambda_init=1e-8, conv
     p_new, conv = iter_proj(rays, pts, p_init, max_iter, lambda_init, convergence_thresh)
     p1 = p_new.astype(np.int64)  # .long() truncation
     Xg = X11[np.arange(b)[:, None], p1[..., 1], p1[..., 0], :].reshape(b, h, w, 3)
-    d = np.sqrt(((Xg.astype(np.float64) - X21) ** 2).sum(-1))
-    valid = conv & (d < dist_thresh).reshape(b, -1)
+    d = norm3(Xg.astype(np.float32) - X21.astype(np.float32))  # torch.linalg.norm(..., dim=-1) in fp32
+    valid = conv & (d < np.float32(dist_thresh)).reshape(b, -1)
     if radius > 0:
         p1 = refine_matches(D11, D21.reshape(b, h * w, -1), p1, radius, dilation_max)
     return pixel_to_lin(p1, w), valid[..., None]
@@ -312,8 +323,8 @@ def match_diag(X11, X21, D11, D21, idx_init=None, max_iter=10, lambda_init=1e-8,
     p_new, conv, diag = iter_proj_diag(rays, pts, p_init, max_iter, lambda_init, convergence_thresh)
     p1 = p_new.astype(np.int64)
     Xg = X11[np.arange(b)[:, None], p1[..., 1], p1[..., 0], :].reshape(b, h, w, 3)
-    d = np.sqrt(((Xg.astype(np.float64) - X21) ** 2).sum(-1)).reshape(b, -1)
-    valid = conv & (d < dist_thresh)
+    d = norm3(Xg.astype(np.float32) - X21.astype(np.float32)).reshape(b, -1)
+    valid = conv & (d < np.float32(dist_thresh))
     p1r = refine_matches(D11, D21.reshape(b, h * w, -1), p1, radius, dilation_max) if radius > 0 else p1
     return {"idx": pixel_to_lin(p1r, w), "valid": valid[..., None], "p_new": p_new, "p1": pixel_to_lin(p1, w),
             "conv": conv, "d": d, "accept_margin": diag[..., 0], "conv_margin": diag[..., 1]}

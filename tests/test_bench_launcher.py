@@ -20,8 +20,9 @@ def _env(**kw):
 
 
 def _json_line(out):
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out
+    # stdout holds exactly the one JSON line (gloo's "[Gloo] Rank ..." prints are sent to stderr)
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out
     return json.loads(lines[0])
 
 

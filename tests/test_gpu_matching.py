@@ -1,7 +1,10 @@
 """GPU parity: matching kernels (iter_proj, refine_matches, fused match) vs the oracle / golden vectors.
 
-Tolerances: p_new within 1e-4 px (FMA/ordering), `converged` and integer
-indices bit-exact except for documented near-integer truncation flips (<= 1e-4 of pixels, SURVEY a-note 4).
+Tolerances: none. The oracle's prep (m3o_normalize3 / m3o_img_gradient) is bit-exact against the reference run's
+torch glue (golden rays / pts), the HIP prep follows the same fp32 FMA order, and the LM iteration, the occlusion
+distance and the c10::Half refine are restated operation for operation: p_new, converged, idx and valid are
+asserted equal, bit for bit (round 6; earlier rounds allowed <= 1e-4 of pixels to flip, which the fp64 oracle prep
+caused: scripts/match_mismatch.py, profiles/r06_match_census.txt).
 """
 import numpy as np
 import pytest
@@ -27,8 +30,8 @@ def test_iter_proj_matches_golden(golden):
     p = p_new.cpu().numpy()
     c = conv.cpu().numpy()
     assert conv.dtype == torch.bool and p_new.dtype == torch.float32
-    np.testing.assert_allclose(p, g["p_new"], atol=1e-4)
-    assert (c != g["converged"]).mean() <= 1e-3
+    np.testing.assert_array_equal(p, g["p_new"])
+    np.testing.assert_array_equal(c, g["converged"])
 
 
 def test_iter_proj_ragged_n():
@@ -42,8 +45,8 @@ def test_iter_proj_ragged_n():
     pts, p_init = pts[:, :n], p_init[:, :n]
     ref_p, ref_c = O.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)
     p_new, conv = B.iter_proj(_dev(rays), _dev(pts), _dev(p_init), 10, 1e-8, 1e-6)
-    np.testing.assert_allclose(p_new.cpu().numpy(), ref_p, atol=1e-4)
-    assert (conv.cpu().numpy() != ref_c).mean() <= 1e-2
+    np.testing.assert_array_equal(p_new.cpu().numpy(), ref_p)
+    np.testing.assert_array_equal(conv.cpu().numpy(), ref_c)
 
 
 @pytest.mark.parametrize("half", [True, False])
@@ -97,11 +100,11 @@ def test_fused_match_matches_golden(golden):
     g = golden("matching_48x64.npz")
     idx, valid = match(_dev(g["X11"]), _dev(g["X21"]), _dev(g["D11"]), _dev(g["D21"]))
     assert idx.shape == (1, 48 * 64) and valid.shape == (1, 48 * 64, 1)
-    assert (idx.cpu().numpy() != g["idx"]).mean() <= 1e-4
-    assert (valid.cpu().numpy() != g["valid"]).mean() <= 1e-4
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["idx"])
+    np.testing.assert_array_equal(valid.cpu().numpy(), g["valid"])
     idx_w, valid_w = match(_dev(g["X11"]), _dev(g["X21"]), _dev(g["D11"]), _dev(g["D21"]), _dev(g["idx_init"]))
-    assert (idx_w.cpu().numpy() != g["idx_warm"]).mean() <= 1e-4
-    assert (valid_w.cpu().numpy() != g["valid_warm"]).mean() <= 1e-4
+    np.testing.assert_array_equal(idx_w.cpu().numpy(), g["idx_warm"])
+    np.testing.assert_array_equal(valid_w.cpu().numpy(), g["valid_warm"])
 
 
 @pytest.mark.parametrize("shape", [(96, 128, 2), (128, 160, 1)])
@@ -117,8 +120,8 @@ def test_fused_match_vs_oracle_batched(shape):
     D21 = np.stack([p["D"][1].numpy() for p in Ps])
     ref_idx, ref_valid = O.match(X11, X21, D11, D21)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
 
 
 @pytest.mark.parametrize("shape,dmax", [((2, 50, 70), 5), ((1, 40, 96), 3), ((1, 64, 64), 8), ((1, 33, 47), 1)])
@@ -137,8 +140,8 @@ def test_fused_match_ragged_and_dilations_vs_oracle(shape, dmax):
     D21 = np.stack([p["D"][1].numpy() for p in Ps])
     ref_idx, ref_valid = O.match(X11, X21, D11, D21, dilation_max=dmax)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
 
 
 @pytest.mark.parametrize("inplace", ["1", "0"])
@@ -159,8 +162,8 @@ def test_fused_match_scattered_warm_start_vs_oracle(monkeypatch, inplace):
     init = np.random.default_rng(3).integers(0, H * W, size=(1, H * W)).astype(np.int64)
     ref_idx, ref_valid = O.match(X11, X21, D11, D21, idx_init=init)
     idx, valid = match(_dev(X11), _dev(X21), _dev(D11), _dev(D21), _dev(init))
-    assert (idx.cpu().numpy() != ref_idx).mean() <= 1e-4
-    assert (valid.cpu().numpy() != ref_valid).mean() <= 1e-4
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+    np.testing.assert_array_equal(valid.cpu().numpy(), ref_valid)
     # reference op on the same scattered centres: bit-exact c10::Half refine
     rays, pts, p_init = O.prep_for_iter_proj(X11, X21, init)
     p_new, _ = O.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)
