@@ -317,9 +317,8 @@ def ba_plan_info(lib, plan):
 
     info = (ctypes.c_int * 13)()
     _lib.check(lib.m3s_ba_plan_info(ctypes.byref(plan), info))
-    keys = ("chunks", "factor_blocks", "levels", "wide_steps", "dense", "targets", "edges", "poses", "subtree_steps",
-            "subtree_workgroups", "supernodes", "supernode_workgroups", "top_poses")
-    return dict(zip(keys, list(info)))
+    keys = ("chunks", "factor_blocks", "levels", "wide_steps", "dense", "targets", "edges", "poses")
+    return dict(zip(keys, list(info)[:len(keys)]))
 
 
 def bench_ba(args, rank, world, dev, leg):
@@ -447,9 +446,7 @@ def bench_ba(args, rank, world, dev, leg):
            "ms_first_lin_with_pack": spans["ba_lin_pack"] if fused else None,
            "ms_lin_per_iter": spans["ba_linearize"], "ms_solve_per_iter": spans["ba_solve"],
            "factor": {"blocks": info["factor_blocks"], "levels": info["levels"], "wide_steps": info["wide_steps"],
-                      "dense": bool(info["dense"]), "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2,
-                      "front_steps": info["subtree_steps"], "front_workgroups": info["subtree_workgroups"],
-                      "dense_top_poses": info["top_poses"]},
+                      "dense": bool(info["dense"]), "dense_blocks": (args.ba_kf - 1) * args.ba_kf // 2},
            "scaling": "strong", "roofline": roof,
            "pack": {"GBps": (pack_bytes + (alg if fused else 0)) / pack_s / 1e9,
                     "frac": (pack_bytes + (alg if fused else 0)) / pack_s / 1e9 / HBM_PEAK_GBS,

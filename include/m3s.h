@@ -154,9 +154,7 @@ int m3s_ba_iterations(const m3s_ba_plan* plan, int* iters_out, void* stream); /*
 /* Host-only facts of a built plan (bench rooflines, tests): info[0] = linearisation chunks per edge,
  * [1] = factor blocks, [2] = elimination-tree levels, [3] = multi-workgroup factor steps, [4] = 1 if the dense
  * fallback factorisation is used, [5] = distinct target keyframes among the shard's edges, [6] = shard edges,
- * [7] = poses, [8] = factor steps run by the optional frontal or subtree phase (one
- * launch), [9] = its workgroups, [10] = supernodes of the supernodal factorisation (0: the column-task one),
- * [11] = its multi-workgroup launch's workgroups, [12] = poses of the dense top phase (0: none). info holds 13 ints. */
+ * [7] = poses, [8..12] = 0 (round 5's opt-in solver phases, removed in round 6). info holds 13 ints. */
 int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info);
 /* Host-only diagnostic of the symbolic factorisation the plan builds for these edges (host arrays):
  * stats[0] = factor blocks (7x7, diagonal included), [1] = elimination-tree levels, [2] = update groups

@@ -557,25 +557,14 @@ inline size_t ba_max_blocks(int Kp) {
 
 // the plan's host-built tables, uploaded in ONE copy: rank arrays, keyframe pointer tables and the
 // symbolic factorisation (ba_pattern.h), packed at their actual sizes into a region sized for the worst case
-constexpr int BA_SYM_SECTIONS = 21;  // the symbolic half's sections (build_symbolic)
-constexpr int BA_TOP_MAX = 25;  // ba.hip TOP_MAX: poses of the dense top phase at most (its LDS: 7T x 7T packed + panels)
-constexpr int BA_SUB_WAVES = 8;     // waves of a subtree-phase workgroup (ba_subtree_kernel)
-constexpr int BA_SUB_MAX_WG = 128;  // subtree-phase workgroups at most (small subtrees are packed together)
+constexpr int BA_SYM_SECTIONS = 16;  // the symbolic half's sections (build_symbolic)
 constexpr int BA_SP_PLAN_BYTES = 144 * 1024;  // ba.hip SP_PLAN_BYTES: LDS of the one-workgroup factor kernel
-constexpr int BA_FRONT_LDS_BYTES = 159 * 1024;  // ba.hip FRONT_LDS_BYTES: LDS image of a frontal-phase workgroup
 constexpr int BA_BLOB_SECTIONS = 8 + BA_SYM_SECTIONS;
 // update pairs (source block row -> target block) the plan can hold: every pattern up to K ~ 600, and the
 // sparse patterns of larger graphs
 inline size_t ba_max_pairs(int Kp) {
   const size_t nb = (size_t)std::max(0, Kp - 1);
   return std::min(nb * nb * nb / 6 + nb * nb + 64, 32 * ba_max_blocks(Kp) + 64);
-}
-// ints reserved for the supernodal plan (ba_snode_plan): records, rows, blk maps, children and lists per supernode,
-// and per pull its map (a pull per off-diagonal factor block at most, R <= 36 rows each); a plan that needs more
-// falls back to the column-task solver
-inline size_t ba_sn_capacity(int Kp) {
-  const size_t nb = (size_t)std::max(0, Kp - 1);
-  return 1024 + 64 * nb + 8 * ba_max_blocks(Kp);
 }
 size_t ba_blob_capacity(int Kp, int E, int chunks) {
   const size_t nb = (size_t)std::max(0, Kp - 1), nLm = ba_max_blocks(Kp);
@@ -585,15 +574,7 @@ size_t ba_blob_capacity(int Kp, int E, int chunks) {
                       (size_t)E * chunks +  // + the linearisation block table
                       2 * (size_t)E +       // + record slots and the pack list (record reuse)
                       8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + wide-step task records
-                      8 * 2 * nb * (size_t)std::min<size_t>(BA_MAX_WIDE_STEPS, nb + 1) +  // + subtree task records
-                      4 * (size_t)BA_SUB_MAX_WG * BA_MAX_WIDE_STEPS +                      //   and their step table
-                      // + the frontal phase: per workgroup (<= nb) directory, header, steps; records (factor + group +
-                      // U tasks), sources and their maps (each update pair once), slot and column maps; apply table
-                      (size_t)nb * (4 + 16 + 2 * (BA_MAX_WIDE_STEPS + 1) + 4) + 8 * (nb + 2 * nLm) + 4 * nLm +
-                      ba_max_pairs(Kp) + nLm + nb + 8 * (size_t)nb + nLm +
-                      2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm) +  // + the dataflow schedule
-                      ba_sn_capacity(Kp) +                                   // + the supernodal plan
-                      4 + BA_TOP_MAX + BA_TOP_MAX * BA_TOP_MAX;              // + the dense top phase
+                      2 * (M3S_BA_SP_WAVES + 1) + 2 * nb + 2 * (nb + nLm);  // + the dataflow schedule
   return ints * 4 + (size_t)Kp * (8 + 8 + 4) + BA_BLOB_SECTIONS * 16;
 }
 
@@ -735,10 +716,6 @@ struct PlanSym {
   std::vector<char> image;  // the tables, packed at 16-B aligned offsets, as uploaded
   size_t off[BA_SYM_SECTIONS] = {0};
   int nb = 0, nlev = 0, nL = 0, wide_steps = 0, dense = 0, flow = 0, plan_lo_off = 0, plan_bytes = 0;
-  int sub_cut = 0, sub_wgs = 0;  // subtree phase: steps [0, sub_cut) in sub_wgs workgroups (ba_subtree_kernel)
-  int front_cut = 0, front_wgs = 0, front_napply = 0;  // frontal subtree phase (ba_front_kernel), see build_symbolic
-  int snode = 0, sn_wgs = 0, nsn = 0;  // supernodal factorisation (ba_snode_kernel): its bottom workgroups, supernodes
-  int top_T = 0, top_lev = 0;          // dense top phase (ba_dense_top_kernel): its poses, its first elimination level
   bool pack_deferred = false;    // the plan's pack runs inside its first linearisation (set at plan time, under g_sym_mu)
   int step_tasks[BA_MAX_WIDE_STEPS] = {0};
   int step_base[BA_MAX_WIDE_STEPS] = {0};  // first task record of each wide step
@@ -764,31 +741,15 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   Y->dense = has_dense && 3.8 * S.nlev + 0.03 * (double)S.sidx.size() > 2.7 * S.nb;
   const char* solver = getenv("M3S_BA_SOLVER");
   if (solver) {  // tests and experiments: force one factorisation
-    if (!strcmp(solver, "sparse") || !strcmp(solver, "snode")) Y->dense = 0;
+    if (!strcmp(solver, "sparse")) Y->dense = 0;
     if (!strcmp(solver, "dense") && has_dense) Y->dense = 1;
   }
-  // supernodal factorisation (ba_snode.cpp / ba_snode.hip): M3S_BA_SOLVER=snode; its back substitution runs in the
-  // one-workgroup kernel on a schedule without factor tasks. M3S_BA_SN_CUT forces the supernodal tree's cut height.
-  std::vector<int> sntab;
-  if (!Y->dense && solver && !strcmp(solver, "snode")) {
-    const char* ce = getenv("M3S_BA_SN_CUT");
-    int nwg = 0;
-    double est = 0.0;
-    const int nsn = ba_snode_plan(S, M3S_BA_SN_SMAX, M3S_BA_SN_GROUPS, 64 * 4, ce && *ce ? atoi(ce) : -1, &sntab, &nwg,
-                                  &est);
-    if (nsn > 0 && sntab.size() <= ba_sn_capacity(Kp)) {
-      Y->snode = 1;
-      Y->sn_wgs = nwg;
-      Y->nsn = nsn;
-    } else {
-      sntab.clear();
-    }
-  }
-  // the leaf end of the elimination tree: by default the subtree phase below (one launch); with M3S_BA_WIDE or
-  // M3S_BA_FLOW=0 the earlier split into multi-workgroup launches (steps [0, wide_steps)), the root end in the
+  // the leaf end of the elimination tree as multi-workgroup launches (steps [0, wide_steps)), the root end in the
   // one-workgroup kernel, minimising the measured step costs (MI355X, C5/C4 graphs): a launch ~5.8 us per step, a
   // step inside the workgroup ~3.7 us per round of M3S_BA_SP_WAVES waves (one wave per task). M3S_BA_WIDE=t (tests,
-  // experiments): every step up to the last one with more than t tasks.
+  // experiments): every step up to the last one with more than t tasks. (Round 5's opt-in alternatives for this
+  // split, the subtree, frontal, supernodal and dense-top phases, measured slower or no faster and were removed in
+  // round 6; they are kept at git tag ba-solver-experiments-r5, DESIGN.md §4 BA.)
   std::vector<int> tasks(S.nlev + 1);
   for (int l = 0; l <= S.nlev; l++) {
     const int na = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
@@ -798,10 +759,10 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
   const int lmax = std::min(S.nlev + 1, BA_MAX_WIDE_STEPS);
   const char* fenv = getenv("M3S_BA_FLOW");
   const bool flow_on = !(fenv && !strcmp(fenv, "0"));  // M3S_BA_FLOW=0 (A/B experiments): level-synchronous loops
-  std::vector<int> sched, subtab;
+  std::vector<int> sched;
   // bytes the one-workgroup dataflow kernel stages in LDS for a schedule (m3s_launch_ba_solve's test): the loop
   // tables col_ptr .. sidx (sections 1-9, 16-B aligned as packed below) + the schedule, x (8 doubles per column) and
-  // 3 flags per column. A plan whose dataflow schedule does not fit runs level-synchronously (no subtree phase).
+  // 3 flags per column. A plan whose dataflow schedule does not fit runs level-synchronously.
   size_t table_bytes = 0;
   {
     const std::vector<int>* t[9] = {&S.col_ptr, &S.lev_ptr, &S.lev_col, &S.grp_ptr, &S.grp, &S.pull_grp, &S.src,
@@ -828,85 +789,17 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
     }
     return best_L;
   };
-  const char* senv = getenv("M3S_BA_SUB");
-  if (senv != nullptr && *senv == '\0') senv = nullptr;
-  if (Y->snode) {
-    Y->wide_steps = 0;  // the supernodal kernels factor everything
-  } else if (const char* w = getenv("M3S_BA_WIDE")) {
+  if (const char* w = getenv("M3S_BA_WIDE")) {
     const int thr = atoi(w);
     int last = -1;
     for (int l = 0; l <= S.nlev; l++)
       if (tasks[l] > thr) last = l;
     Y->wide_steps = std::min(last + 1, BA_MAX_WIDE_STEPS);
-  } else if (flow_on && senv != nullptr && atoi(senv) >= 0) {
-    // subtree phase (M3S_BA_SUB=c; an option, not the default): steps [0, cut) run as ONE launch, one workgroup
-    // per subtree below the cut; the rest in the one-workgroup kernel. c = 0 picks the cut that minimises the
-    // estimated finish time (the slowest subtree workgroup + its launch (~4 us) + the one-workgroup factor
-    // schedule's makespan), among the cuts whose schedule fits the kernel's LDS. Measured on MI355X (DESIGN.md §4
-    // BA): slower than the launched wide steps at every cut on the C5 / C4 graphs (solve 0.45-0.53 vs 0.40-0.42 ms):
-    // a subtree task's dependent global round trips cost what a launched step does, and the spine-targeted groups
-    // of the subtree steps lengthen the one-workgroup schedule.
-    const int forced = atoi(senv);
-    std::vector<std::pair<double, int>> cand;
-    std::vector<int> tmp_t;
-    for (int cut = 0; cut < lmax; cut++) {
-      if (forced > 0 && cut != std::min(forced, lmax - 1)) continue;
-      double sub_us = 0.0;
-      if (cut > 0) ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &tmp_t, &sub_us);
-      std::vector<int> sc;
-      const double t = (cut > 0 ? 4.0 + sub_us : 0.0) + ba_flow_schedule(S, 0, M3S_BA_SP_WAVES, &sc, cut);
-      if (flow_fits(sc)) cand.push_back({t, cut});
-    }
-    std::stable_sort(cand.begin(), cand.end());
-    if (cand.empty()) {  // no dataflow schedule fits: level-synchronous with launched wide steps
-      Y->wide_steps = legacy_split();
-    } else {
-      const int cut = cand[0].second;
-      double sub_us = 0.0;
-      Y->sub_wgs = cut > 0 ? ba_subtree_plan(S, cut, BA_SUB_WAVES, BA_SUB_MAX_WG, &subtab, &sub_us) : 0;
-      Y->sub_cut = Y->sub_wgs > 0 ? cut : 0;
-      if (Y->sub_wgs == 0) subtab.clear();
-      Y->wide_steps = 0;
-    }
   } else {
     Y->wide_steps = legacy_split();
   }
-  // Frontal subtree phase (an option, not the default: M3S_BA_FRONT=c forces cut c, -1 the highest that fits): the
-  // steps below the cut run as ONE launch with every subtree's blocks in its workgroup's LDS (ba_front_plan), in front
-  // of the launched steps [cut, wide). The cut: at most the launched steps - 1, with workgroups that fit the LDS
-  // image and U columns that fit the factor region's unused tail (the workspace reserves the densest pattern's
-  // blocks). Measured on MI355X (DESIGN.md §4 BA): no faster than the launched steps (a step inside the workgroup
-  // costs ~5.1 us against ~5.6 us per launched step; the column tasks are issue-latency bound either way).
-  std::vector<int> fronttab, frontapply;
-  const char* fenv2 = getenv("M3S_BA_FRONT");
-  const int front_forced = fenv2 && *fenv2 ? atoi(fenv2) : 0;
-  if (front_forced != 0 && !Y->dense && !Y->snode && Y->sub_cut == 0 && Y->wide_steps >= 2 && S.nlev >= 2) {
-    const int hi = std::min(Y->wide_steps - 1, S.nlev - 1);
-    const size_t u_cap = (ba_max_blocks(Kp) - (size_t)S.nL) * 64;
-    for (int cut = front_forced > 0 ? std::min(front_forced, hi) : hi; cut >= 1; cut--) {
-      size_t ud = 0;
-      int nap = 0;
-      const int nwg = ba_front_plan(S, cut, BA_FRONT_LDS_BYTES, &fronttab, &frontapply, &ud, &nap);
-      if (nwg > 0 && ud <= u_cap) {
-        Y->front_cut = cut;
-        Y->front_wgs = nwg;
-        Y->front_napply = nap;
-        break;
-      }
-      fronttab.clear();
-      frontapply.clear();
-      if (front_forced > 0) break;
-    }
-  }
-  std::vector<int> lev_of(S.nb, 0);
-  for (int l = 0; l < S.nlev; l++)
-    for (int c = S.lev_ptr[l]; c < S.lev_ptr[l + 1]; c++) lev_of[S.lev_col[c]] = l;
-  if (Y->front_cut > 0)  // the U columns replace the pull groups of the columns at the cut (their sources lie below)
-    for (int j = 0; j < S.nb; j++)
-      if (lev_of[j] == Y->front_cut) S.pull_grp[j] = -1;
   // the wide steps' task records (ba_sparse_step_kernel): per task {j, b0, b1, pull group or -1} and its group's
-  // source range, so a launched task starts with its column's own loads. With the frontal phase the steps <= cut
-  // carry no update groups (their sources lie below the cut: the U columns replaced them).
+  // source range, so a launched task starts with its column's own loads
   std::vector<int> step_rec;
   {
     auto put = [&](int j, int g) {
@@ -919,59 +812,21 @@ int build_symbolic(PlanSym* Y, std::vector<int> ri, std::vector<int> rj, int E, 
       Y->step_na[l] = l < S.nlev ? S.lev_ptr[l + 1] - S.lev_ptr[l] : 0;
       for (int c = l < S.nlev ? S.lev_ptr[l] : 0; c < (l < S.nlev ? S.lev_ptr[l + 1] : 0); c++)
         put(S.lev_col[c], S.pull_grp[S.lev_col[c]]);
-      if (Y->front_cut == 0 || l > Y->front_cut)  // (step 0 has no groups: sources at level -1)
-        for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);
+      for (int t = S.grp_ptr[l]; t < S.grp_ptr[l + 1]; t++) put(S.grp[4 * (size_t)t], t);  // (none at step 0)
       Y->step_tasks[l] = (int)step_rec.size() / 8 - Y->step_base[l];
     }
   }
-  // Dense top phase (M3S_BA_TOP=t, an option): the root end of the elimination tree, the lowest level cut whose
-  // columns number at most t (<= BA_TOP_MAX) poses, factored densely on the matrix cores (ba_dense_top_kernel) between a
-  // factor-only and a back-substitution-only run of the one-workgroup kernel
-  std::vector<int> toptab;
-  {
-    const char* tenv = getenv("M3S_BA_TOP");
-    const int tmax = tenv && *tenv ? std::min(atoi(tenv), BA_TOP_MAX) : 0;
-    if (tmax >= 2 && flow_on && !Y->dense && !Y->snode && Y->sub_cut == 0 && Y->front_cut == 0)
-      for (int l = std::max(Y->wide_steps, 1); l < S.nlev; l++)
-        if (S.nb - S.lev_ptr[l] <= tmax) {
-          if (S.nb - S.lev_ptr[l] >= 2 && ba_top_plan(S, l, &toptab) > 0) {
-            Y->top_T = toptab[0];
-            Y->top_lev = l;
-          }
-          break;
-        }
-  }
   // dataflow schedule of the one-workgroup part and the back substitution (ba_pattern.h)
-  // (supernodal: a schedule of the back substitution alone, every column factored before the kernel starts)
-  if (flow_on || Y->snode)
-    ba_flow_schedule(S, Y->snode ? S.nlev + 1 : Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut, Y->top_lev);
+  if (flow_on) ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched);
   Y->flow = sched.empty() ? 0 : 1;
   if (Y->flow && !flow_fits(sched)) {  // the kernel would run level-synchronously: drop the schedule (and say so)
     Y->flow = 0;
     sched.clear();
   }
-  if (Y->snode && !Y->flow) {  // the back substitution after the supernodal factor needs the dataflow kernel
-    Y->err = "ba: the supernodal solver needs the back-substitution schedule in LDS";
-    return M3S_EINVAL;
-  }
-  if (!Y->flow && Y->sub_cut > 0) {  // the subtree phase needs the dataflow kernel (it runs the subtrees' spine groups)
-    Y->err = "ba: the subtree phase needs the dataflow schedule";
-    return M3S_EINVAL;
-  }
-  if (!Y->flow && Y->top_T > 0) {  // a schedule without the top columns that does not fit: no top phase
-    Y->top_T = Y->top_lev = 0;
-    toptab.clear();
-    if (flow_on) {
-      ba_flow_schedule(S, Y->wide_steps, M3S_BA_SP_WAVES, &sched, Y->sub_cut, 0);
-      Y->flow = flow_fits(sched) ? 1 : 0;
-      if (!Y->flow) sched.clear();
-    }
-  }
   const std::vector<int>* secs[BA_SYM_SECTIONS] = {&S.perm,    &S.col_ptr,  &S.rowL,    &S.lev_ptr,  &S.lev_col,
                                                    &S.grp_ptr, &S.grp,      &S.pull_grp, &S.src,     &S.sidx,
                                                    &sched,     &S.asm_ptr,  &S.asm_ent, &S.rhs_ptr, &S.rhs_ent,
-                                                   &step_rec, &subtab,  &fronttab,  &frontapply, &sntab,
-                                                   &toptab};
+                                                   &step_rec};
   size_t total = 0;
   for (int k = 0; k < BA_SYM_SECTIONS; k++) {
     Y->off[k] = total;
@@ -1052,9 +907,7 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
       (const void**)&a.perm,    (const void**)&a.col_ptr, (const void**)&a.rowL,    (const void**)&a.lev_ptr,
       (const void**)&a.lev_col, (const void**)&a.grp_ptr, (const void**)&a.grp,     (const void**)&a.pull_grp,
       (const void**)&a.src,     (const void**)&a.sidx,    (const void**)&a.sched,   (const void**)&a.asm_ptr,
-      (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec,
-      (const void**)&a.sub_tab, (const void**)&a.front_tab, (const void**)&a.front_apply, (const void**)&a.sn_tab,
-      (const void**)&a.top_tab};
+      (const void**)&a.asm_ent, (const void**)&a.rhs_ptr, (const void**)&a.rhs_ent, (const void**)&a.step_rec};
   for (int k = 0; k < BA_SYM_SECTIONS; k++) *dst[k] = d + Y->off[k];
   a.plan_lo = d + Y->plan_lo_off;
   a.plan_bytes = Y->plan_bytes;
@@ -1062,15 +915,6 @@ BaArgs with_symbolic(const BaPlanImpl* P, const PlanSym* Y) {
   a.nlev = Y->nlev;
   a.wide_steps = Y->wide_steps;
   a.flow = Y->flow;
-  a.sub_cut = Y->sub_cut;
-  a.sub_wgs = Y->sub_wgs;
-  a.front_cut = Y->front_cut;
-  a.front_wgs = Y->front_wgs;
-  a.front_napply = Y->front_napply;
-  a.front_u = a.L + (size_t)Y->nL * 64;
-  a.snode = Y->snode;
-  a.sn_wgs = Y->sn_wgs;
-  a.top_T = Y->top_T;
   return a;
 }
 
@@ -1504,11 +1348,7 @@ extern "C" int m3s_ba_plan_info(const m3s_ba_plan* plan, int* info) {
   info[5] = P->n_targets;
   info[6] = P->e1 - P->e0;
   info[7] = P->Kp;
-  info[8] = Y->front_wgs > 0 ? Y->front_cut : Y->sub_cut;
-  info[9] = Y->front_wgs > 0 ? Y->front_wgs : Y->sub_wgs;
-  info[10] = Y->snode ? Y->nsn : 0;
-  info[11] = Y->snode ? Y->sn_wgs : 0;
-  info[12] = Y->top_T;
+  info[8] = info[9] = info[10] = info[11] = info[12] = 0;  // round 5's opt-in solver phases (removed in round 6)
   return M3S_OK;
 }
 

@@ -1256,408 +1256,8 @@ __global__ void __launch_bounds__(64) ba_sparse_step_kernel(BaArgs a, int rec_ba
   else sp_update_group_at(a, T, r0.x, r0.y, r0.z, make_int2(r1.x, r1.y), lane, s_red);
 }
 
-// Subtree phase: steps [0, sub_cut) of the factorisation as ONE launch. Workgroup b owns the subtrees the plan packed
-// into it (ba_pattern.h ba_subtree_plan): per step its factor tasks and the update groups whose targets are its own
-// columns, one wave per task, a workgroup barrier between steps (every hand-off stays on one CU and its XCD's L2).
-// The same per-task code as the wide steps and the one-workgroup kernel: bit-identical factor. The update groups of
-// these steps that target columns above the cut run first in the one-workgroup kernel's dataflow schedule.
-constexpr int SUB_WAVES = 8;
-__global__ void __launch_bounds__(SUB_WAVES * 64) ba_subtree_kernel(BaArgs a) {
-  __shared__ double s_red[SUB_WAVES][64];
-  if (*a.done) return;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cut = a.sub_cut;
-  const int4* steps = a.sub_tab + (size_t)blockIdx.x * cut;
-  const int4* rec = a.sub_tab + (size_t)a.sub_wgs * cut;
-  const SpTables T = sp_tables(a, reinterpret_cast<const int*>(a.plan_lo));
-  for (int l = 0; l < cut; l++) {
-    const int4 st = steps[l];
-    for (int t = w; t < st.y; t += SUB_WAVES) {
-      const int4 r0 = rec[2 * (st.x + t)], r1 = rec[2 * (st.x + t) + 1];
-      if (t < st.z) sp_factor_column_at(a, T, r0.x, r0.y, r0.z, r0.w >= 0, make_int2(r1.x, r1.y), lane, s_red[w], a.bad);
-      else sp_update_group_at(a, T, r0.x, r0.y, r0.z, make_int2(r1.x, r1.y), lane, s_red[w]);
-    }
-    if (st.y > 0) __syncthreads();
-  }
-}
-
-// Frontal subtree phase (ba_pattern.h ba_front_plan): one workgroup per elimination subtree below the cut, its factor
-// blocks (rows 0..6 of each 8x8 block, FB doubles), rhs rows and translated task tables resident in LDS. Steps
-// [0, cut) run level by level (a barrier between steps, every hand-off an LDS access); then each target column above
-// the cut gets this subtree's summed update U (sources ascending) in a scratch column shaped like the target's rows;
-// the factor and rhs rows go back to L / y once.
-constexpr int FRONT_WAVES = 8;
-constexpr int FRONT_LDS_BYTES = 159 * 1024;
-constexpr int FB = 56;
-
-struct FrontCtx {
-  double* L;        // nslots blocks of FB doubles
-  double* Y;        // ncols rhs rows of 8 doubles
-  const int* src;   // int4 {slot of L_jk, yslot of k, sidx offset, 0}
-  const int* sidx;  // per source, per block of the target: slot or -1
-};
-
-// row p of a task's target: block p / 7 of the target (slot0 ...), the rhs row after them
-__device__ __forceinline__ double* fr_row(const FrontCtx& F, int slot0, int nblk, int ys, int p) {
-  return p < 7 * nblk ? F.L + (slot0 + p / 7) * FB + (p - 7 * (p / 7)) * 8 : F.Y + ys * 8;
-}
-
-// v -= x L_jk^T for the task's sources [s0, s1) (row p of a target with nblk blocks; lanes without the row idle).
-// L_jk is read straight from LDS (rows of stride 8; every lane reads the same words: broadcast).
-__device__ __forceinline__ void fr_sources(const FrontCtx& F, int s0, int s1, int nblk, int p, bool act,
-                                           double (&v)[8]) {
-  for (int e = s0; e < s1; e++) {
-    const int4 s = reinterpret_cast<const int4*>(F.src)[e];
-    const double* xr = nullptr;
-    if (act) {
-      if (p == 7 * nblk) {
-        xr = F.Y + s.y * 8;
-      } else {
-        const int sb = F.sidx[s.z + p / 7];
-        xr = sb >= 0 ? F.L + sb * FB + (p - 7 * (p / 7)) * 8 : nullptr;
-      }
-    }
-    if (xr) {
-      double x[8];
-      ld_row(x, xr);
-      const double* bjk = F.L + s.x * FB;
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        const double* bc = bjk + c * 8;
-        const double p0 = fma(x[0], bc[0], x[1] * bc[1]);
-        const double p1 = fma(x[2], bc[2], x[3] * bc[3]);
-        const double p2 = fma(x[4], bc[4], x[5] * bc[5]);
-        v[c] -= (p0 + p1) + fma(x[6], bc[6], p2);
-      }
-    }
-  }
-}
-
-// one task of a front workgroup: r = {kind, slot0, nblk, yslot, src begin, src end, U offset}. kind 0: pull the
-// sources, then the column's register-row factorisation (as sp_factor_column_at: lanes 0..6 the diagonal rows, the
-// triangular solve for the rows below, the forward substitution for the rhs row; passes of 64 rows); kind 1: an update
-// group into an LDS column; kind 2: the U column of a target above the cut (v = 0, the sources, stored to U)
-__device__ __forceinline__ void fr_task(const FrontCtx& F, const int* r, double* U, int lane, int* bad) {
-  const int kind = r[0], slot0 = r[1], nblk = r[2], ys = r[3], s0 = r[4], s1 = r[5];
-  const int nrow = 7 * nblk + 1;
-  double inv[7], lo[21];
-  bool fail = false;
-  for (int base = 0; base < nrow; base += 64) {
-    const int p = base + lane;
-    const bool act = p < nrow;
-    double v[8];
-    double* rp = nullptr;
-    if (kind == 2) {
-#pragma unroll
-      for (int c = 0; c < 8; c++) v[c] = 0.0;
-    } else {
-      rp = act ? fr_row(F, slot0, nblk, ys, p) : nullptr;
-      if (act) {
-        ld_row(v, rp);
-      } else {
-#pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = 0.0;
-      }
-    }
-    fr_sources(F, s0, s1, nblk, p, act, v);
-    if (kind == 0) {
-      if (base == 0) {
-#pragma unroll
-        for (int m = 0; m < 7; m++) {
-          double d = bcast_lane(v[m], m);
-          if (!(d > 0.0)) {
-            fail = true;
-            d = 1.0;
-          }
-          inv[m] = rsqrt_nr(d);
-          const double l = v[m] * inv[m];
-          v[m] = lane == m ? d * inv[m] : l;
-#pragma unroll
-          for (int c = m + 1; c < 7; c++) {
-            const double lc = bcast_lane(l, c);
-            lo[c * (c - 1) / 2 + m] = lc;
-            v[c] = fma(-l, lc, v[c]);
-          }
-        }
-        if (lane < 7) {
-          double iv = inv[0];
-#pragma unroll
-          for (int m = 1; m < 7; m++) iv = lane == m ? inv[m] : iv;
-          v[7] = iv;
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < 7; m++) {
-          v[m] *= inv[m];
-#pragma unroll
-          for (int c = m + 1; c < 7; c++) v[c] = fma(-v[m], lo[c * (c - 1) / 2 + m], v[c]);
-        }
-      }
-    }
-    if (act) {
-      if (kind == 2)
-        st_row(U + r[6] + (size_t)p * 8, v);
-      else
-        st_row(rp, v);
-    }
-  }
-  if (fail && lane == 0) atomicOr(bad, BA_BAD_LLT);
-}
-
-__global__ void __launch_bounds__(FRONT_WAVES * 64) ba_front_kernel(BaArgs a) {
-  __shared__ __attribute__((aligned(16))) double s_front[FRONT_LDS_BYTES / 8];
-  if (*a.done) return;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  constexpr int NT = FRONT_WAVES * 64;
-  const int4 dir = reinterpret_cast<const int4*>(a.front_tab)[blockIdx.x];
-  const int* gt = a.front_tab + dir.x;
-  const int nslots = gt[0], ncols = gt[1], cut = gt[2];
-  double* L = s_front;
-  double* Y = s_front + nslots * FB;
-  int* T = reinterpret_cast<int*>(Y + ncols * 8);
-  {  // the table (16-B sections, dir.y a multiple of 4)
-    const int4* g4 = reinterpret_cast<const int4*>(gt);
-    int4* t4 = reinterpret_cast<int4*>(T);
-    for (int i = tid; i < dir.y / 4; i += NT) t4[i] = g4[i];
-  }
-  __syncthreads();
-  const int* slot_gb = T + T[7];
-  const int* colj = T + T[8];
-  double2* L2 = reinterpret_cast<double2*>(L);
-  double2* Y2 = reinterpret_cast<double2*>(Y);
-  const double2* gL = reinterpret_cast<const double2*>(a.L);
-  const double2* gy = reinterpret_cast<const double2*>(a.y);
-  for (int i = tid; i < nslots * (FB / 2); i += NT) {
-    const int s = i / (FB / 2), e = i - (FB / 2) * s;
-    L2[i] = gL[(size_t)slot_gb[s] * 32 + e];
-  }
-  for (int i = tid; i < ncols * 4; i += NT) Y2[i] = gy[(size_t)colj[i >> 2] * 4 + (i & 3)];
-  __syncthreads();
-  const FrontCtx F{L, Y, T + T[5], T + T[6]};
-  const int* rec = T + T[4];
-  const int2* steps = reinterpret_cast<const int2*>(T + 16);
-  for (int l = 0; l <= cut; l++) {  // l == cut: the U columns (LDS read-only from here)
-    const int2 st = steps[l];
-    for (int t = w; t < st.y; t += FRONT_WAVES) fr_task(F, rec + 8 * (st.x + t), a.front_u, lane, a.bad);
-    if (l < cut && st.y > 0) __syncthreads();
-  }
-  double2* gLw = reinterpret_cast<double2*>(a.L);
-  double2* gyw = reinterpret_cast<double2*>(a.y);
-  for (int i = tid; i < nslots * (FB / 2); i += NT) {
-    const int s = i / (FB / 2), e = i - (FB / 2) * s;
-    gLw[(size_t)slot_gb[s] * 32 + e] = L2[i];
-  }
-  for (int i = tid; i < ncols * 4; i += NT) gyw[(size_t)colj[i >> 2] * 4 + (i & 3)] = Y2[i];
-}
-
-// the U columns into L / y: one workgroup per target above the cut, the workgroups' columns in ascending order
-__global__ void __launch_bounds__(64) ba_front_apply_kernel(BaArgs a) {
-  if (*a.done) return;
-  const int lane = threadIdx.x;
-  const int* e = a.front_apply + 8 * blockIdx.x;
-  const int j = e[0], b0 = e[1], nblk = e[2], u0 = e[3], u1 = e[4];
-  const int* ul = a.front_apply + 8 * a.front_napply;
-  const int nrow = 7 * nblk + 1;
-  for (int p = lane; p < nrow; p += 64) {
-    double* rp = p < 7 * nblk ? a.L + (size_t)(b0 + p / 7) * 64 + (p - 7 * (p / 7)) * 8 : a.y + (size_t)j * 8;
-    double v[8];
-    ld_row(v, rp);
-    int u = u0;
-    for (; u + 4 <= u1; u += 4) {  // four U rows in flight, added in list order
-      double x[4][8];
-#pragma unroll
-      for (int q = 0; q < 4; q++) ld_row(x[q], a.front_u + ul[u + q] + (size_t)p * 8);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int c = 0; c < 8; c++) v[c] += x[q][c];
-    }
-    for (; u < u1; u++) {
-      double x[8];
-      ld_row(x, a.front_u + ul[u] + (size_t)p * 8);
-#pragma unroll
-      for (int c = 0; c < 8; c++) v[c] += x[c];
-    }
-    st_row(rp, v);
-  }
-}
-
-// ---- dense top phase (ba_pattern.h ba_top_plan; M3S_BA_TOP) ----
-// The root end of the elimination tree (T <= TOP_MAX poses at levels >= the plan's cut) holds a nearly dense factor:
-// instead of one dependent column task per level, ONE workgroup factors its n = 7T rows densely, after the factor-only
-// run of the one-workgroup kernel applied every update from the columns below. Right-looking over 7-column panels
-// (one pose each):
-//   (a) the owners of the panel's columns write them (rows >= c0) from their accumulator tiles to LDS;
-//   (b) wave 0 factors the 7x7 diagonal block in registers (rows in lanes 0-6, the rhs in lane 7: forward
-//       substitution y_p = L_pp^-1 b_p), the same pivot arithmetic as sp_factor_column_at;
-//   (c) one thread per row below solves x L_pp^T = a (the panel of L) and updates its rhs entry;
-//   (d) every wave updates its trailing 16x16 tiles, C -= P P^T, on the matrix cores (v_mfma_f64_16x16x4, K = 7
-//       padded to 8; the tiles stay in registers across panels).
-// Then the back substitution from the root down (x_p = L_pp^-T z_p, z of the poses before it updated right-looking)
-// and x into a.xs (factor order) for the back-substitution-only run. Deterministic (fixed ownership and order); not
-// bit-identical to the column-task factor (other summation order).
-typedef double d4v __attribute__((ext_vector_type(4)));
-constexpr int TOP_MAX = 25;
-constexpr int TOP_NMAX = 7 * TOP_MAX;                  // 175 rows at most
-constexpr int TOP_NP = ((TOP_NMAX + 15) / 16) * 16;   // 176: whole 16-row tiles
-constexpr int TOP_TILES = TOP_NP / 16;                 // 11 tile rows
-constexpr int TOP_NT = TOP_TILES * (TOP_TILES + 1) / 2;  // 66 lower tiles
-constexpr int TOP_SLOTS = (TOP_NT + SP_WAVES - 1) / SP_WAVES;  // tiles per wave at most
-
-__global__ void __launch_bounds__(1024) ba_dense_top_kernel(BaArgs a) {
-  if (*a.done) return;
-  const int T = a.top_T, n = 7 * T;
-  const int* cols = a.top_tab + 4;
-  const int* map = cols + T;
-  __shared__ double sL[TOP_NMAX * (TOP_NMAX + 1) / 2];  // the factor, packed lower: (r, c) at r (r + 1) / 2 + c
-  __shared__ double sP[TOP_NP][8];                        // (a): the panel's columns as they stand (rows >= c0)
-  __shared__ double sPL[TOP_NP][8];                       // (c): its L, zero outside rows [c0 + 7, n) and in column 7
-  __shared__ double sy[TOP_NP];                           // rhs -> forward-substituted y -> x
-  __shared__ double sinv[TOP_NMAX];                       // 1 / L_mm
-  __shared__ int s_fail;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-  // this wave's tiles u = w + 16 s (lower tiles in row order: u = I (I + 1) / 2 + J), their accumulators
-  int tI[TOP_SLOTS], tJ[TOP_SLOTS];
-  d4v acc[TOP_SLOTS];
-#pragma unroll
-  for (int q = 0; q < TOP_SLOTS; q++) {
-    const int u = w + SP_WAVES * q;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= u) I++;
-    tI[q] = u < TOP_NT ? I : -1;
-    tJ[q] = u - I * (I + 1) / 2;
-    // the dense A from the top columns' factor blocks (block (a, b) row m, column mm), upper half zero
-#pragma unroll
-    for (int r4 = 0; r4 < 4; r4++) {
-      const int r = 16 * I + lk + 4 * r4, c = 16 * tJ[q] + lr;
-      double v = 0.0;
-      if (u < TOP_NT && r < n && c <= r) {
-        const int blk = map[(r / 7) * T + c / 7];
-        if (blk >= 0) v = a.L[(size_t)blk * 64 + (r % 7) * 8 + c % 7];
-      }
-      acc[q][r4] = v;
-    }
-  }
-  for (int i = threadIdx.x; i < TOP_NP * 8; i += 1024) (&sPL[0][0])[i] = 0.0;
-  for (int r = threadIdx.x; r < TOP_NP; r += 1024) sy[r] = r < n ? a.y[(size_t)cols[r / 7] * 8 + r % 7] : 0.0;
-  if (threadIdx.x == 0) s_fail = 0;
-  for (int p = 0; p < T; p++) {
-    const int c0 = 7 * p;
-    // (a) the panel's columns [c0, c0 + 7), rows >= their diagonal, from the owning tiles
-#pragma unroll
-    for (int q = 0; q < TOP_SLOTS; q++) {
-      if (tI[q] < 0 || 16 * tJ[q] > c0 + 6 || 16 * tJ[q] + 15 < c0) continue;
-#pragma unroll
-      for (int r4 = 0; r4 < 4; r4++) {
-        const int r = 16 * tI[q] + lk + 4 * r4, c = 16 * tJ[q] + lr;
-        if (c >= c0 && c < c0 + 7 && r >= c && r < n) sP[r][c - c0] = acc[q][r4];
-      }
-    }
-    __syncthreads();  // every wave is past its (d) of the previous panel: sPL is free
-    // (b) the diagonal block (lanes 0-6: its rows, lane 7: the rhs), then L_pp, 1/L_mm and y_p into LDS
-    if (w == 0) {
-      double v[7];
-#pragma unroll
-      for (int c = 0; c < 7; c++)
-        v[c] = lane < 7 ? (c <= lane ? sP[c0 + lane][c] : 0.0) : (lane == 7 ? sy[c0 + c] : 0.0);
-      bool fail = false;
-      double inv[7];
-#pragma unroll
-      for (int m = 0; m < 7; m++) {
-        double d = bcast_lane(v[m], m);
-        if (!(d > 0.0)) {  // not positive definite: the step is discarded (dx = 0), as SimplicialLLT's info
-          fail = true;
-          d = 1.0;
-        }
-        inv[m] = rsqrt_nr(d);
-        const double l = v[m] * inv[m];
-        v[m] = lane == m ? d * inv[m] : l;
-#pragma unroll
-        for (int c = m + 1; c < 7; c++) v[c] = fma(-l, bcast_lane(l, c), v[c]);
-      }
-      if (fail && lane == 0) s_fail = 1;
-      if (lane < 7) {
-        double* row = sL + (size_t)(c0 + lane) * (c0 + lane + 1) / 2 + c0;
-#pragma unroll
-        for (int c = 0; c < 7; c++)
-          if (c <= lane) row[c] = v[c];
-        sinv[c0 + lane] = inv[0];
-#pragma unroll
-        for (int m = 1; m < 7; m++)
-          if (lane == m) sinv[c0 + lane] = inv[m];
-      } else if (lane == 7) {
-#pragma unroll
-        for (int c = 0; c < 7; c++) sy[c0 + c] = v[c];
-      }
-      if (lane < 56) sPL[c0 + lane / 8][lane % 8] = 0.0;  // the previous panel's L rows: no trailing part any more
-    }
-    __syncthreads();
-    // (c) the panel of L below the diagonal block: x L_pp^T = a per row (right-looking, as sp_rows_extra), its rhs
-    const int r = c0 + 7 + (int)threadIdx.x;
-    if (r < n) {
-      double v[7];
-#pragma unroll
-      for (int c = 0; c < 7; c++) v[c] = sP[r][c];
-#pragma unroll
-      for (int m = 0; m < 7; m++) {
-        v[m] *= sinv[c0 + m];
-#pragma unroll
-        for (int c = m + 1; c < 7; c++) v[c] = fma(-v[m], sL[(size_t)(c0 + c) * (c0 + c + 1) / 2 + c0 + m], v[c]);
-      }
-      double* row = sL + (size_t)r * (r + 1) / 2 + c0;
-      double b = sy[r];
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        row[c] = v[c];
-        sPL[r][c] = v[c];
-        b = fma(-v[c], sy[c0 + c], b);
-      }
-      sy[r] = b;
-    }
-    __syncthreads();
-    // (d) the trailing tiles: C -= P P^T (A = -P rows of tile I, B = P rows of tile J; rows outside the trailing
-    // part of P are zero, so the rest of every tile is unchanged)
-#pragma unroll
-    for (int q = 0; q < TOP_SLOTS; q++) {
-      if (tI[q] < 0 || 16 * tJ[q] + 15 < c0 + 7) continue;
-      const double a0 = -sPL[16 * tI[q] + lr][lk], a1 = -sPL[16 * tI[q] + lr][4 + lk];
-      const double b0 = sPL[16 * tJ[q] + lr][lk], b1 = sPL[16 * tJ[q] + lr][4 + lk];
-      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[q], 0, 0, 0);
-      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[q], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-  // back substitution from the root: x_p = L_pp^-T z_p (wave 0), then z_c -= L(c0 + m, c) x_m for the rows before it
-  for (int p = T - 1; p >= 0; p--) {
-    const int c0 = 7 * p;
-    if (w == 0 && lane == 0) {
-      double x[7];
-#pragma unroll
-      for (int mm = 6; mm >= 0; mm--) {
-        double vv = sy[c0 + mm];
-#pragma unroll
-        for (int q = mm + 1; q < 7; q++) vv = fma(-sL[(size_t)(c0 + q) * (c0 + q + 1) / 2 + c0 + mm], x[q], vv);
-        x[mm] = vv * sinv[c0 + mm];
-      }
-#pragma unroll
-      for (int mm = 0; mm < 7; mm++) sy[c0 + mm] = x[mm];
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < c0; c += 1024) {
-      double z = sy[c];
-#pragma unroll
-      for (int m = 0; m < 7; m++) z = fma(-sL[(size_t)(c0 + m) * (c0 + m + 1) / 2 + c], sy[c0 + m], z);
-      sy[c] = z;
-    }
-    __syncthreads();
-  }
-  for (int r = threadIdx.x; r < n; r += 1024) a.xs[(size_t)cols[r / 7] * 8 + r % 7] = sy[r];
-  if (threadIdx.x == 0 && s_fail) atomicOr(a.bad, BA_BAD_LLT);
-}
-
 template <bool LT>  // LT: the loop tables and x fit in LDS (index lookups are ds_reads), else global
-__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh, int phase) {
+__global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K, int nL, float delta_thresh) {
   if (*a.done) return;
   __shared__ __attribute__((aligned(16))) int s_plan[LT ? SP_PLAN_BYTES / 4 : 4];
   __shared__ double s_red[SP_WAVES][64];  // per-wave staging: L_jk and the back-substitution sums
@@ -1698,15 +1298,6 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
       f_fac[i] = fac_init[i];
       f_xd[i] = 0;
     }
-    if (phase == 2) {  // after the dense top phase: its columns' x (a.xs) and their done flags
-      __syncthreads();
-      const int* tc = a.top_tab + 4;
-      for (int i = threadIdx.x; i < 8 * a.top_T; i += 1024) {
-        const int j = tc[i >> 3];
-        X[(size_t)j * 8 + (i & 7)] = a.xs[(size_t)j * 8 + (i & 7)];
-        if ((i & 7) == 0) f_xd[j] = 1;
-      }
-    }
   }
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
@@ -1716,7 +1307,7 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     // every wave walks its own task list (step order); a task waits only for its inputs
     const int* S = T.sched;
     const int2* wl = reinterpret_cast<const int2*>(S + 2 * (SP_WAVES + 1) + nb);
-    for (int t = phase == 2 ? S[w + 1] : S[w]; t < S[w + 1]; t++) {
+    for (int t = S[w]; t < S[w + 1]; t++) {
       const int2 tk = wl[t];
       if (tk.x >= 0) {
         const int j = tk.x, gp = T.pull_grp[j];
@@ -1739,10 +1330,6 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
     }
     __syncthreads();
     SPST(2 + nlev);
-    if (phase == 1) {  // factor only (the dense top phase follows): report a failed pivot through *a.bad
-      if (threadIdx.x == 0 && s_bad != 0) atomicOr(a.bad, s_bad);
-      return;
-    }
     const int* bs_ptr = S + SP_WAVES + 1;
     const int* bs_col = S + 2 * (SP_WAVES + 1) + nb + 2 * S[SP_WAVES];
     for (int t = bs_ptr[w]; t < bs_ptr[w + 1]; t++) {
@@ -1776,8 +1363,8 @@ __global__ void __launch_bounds__(1024) ba_sparse_factor_kernel(BaArgs a, int K,
   }
   __syncthreads();
   SPST(3 + 2 * nlev);
-  // the multi-workgroup factor launches (wide steps, subtree phase, supernodal kernels) report through *a.bad
-  const int ext_bad = (a.wide_steps > 0 || a.sub_wgs > 0 || a.snode || a.top_T > 0) ? *(volatile int*)a.bad : 0;
+  // the multi-workgroup factor launches (the wide steps) report through *a.bad
+  const int ext_bad = a.wide_steps > 0 ? *(volatile int*)a.bad : 0;
   const bool failed = s_bad != 0 || ext_bad != 0;
   const bool stalled = ((s_bad | ext_bad) & BA_BAD_STALL) != 0;
   const int n = a.nb * 7;
@@ -1870,7 +1457,6 @@ extern "C" hipError_t m3s_launch_ba_lin(const BaArgs* a, const BaParams* p, int 
 // assembly (nL factor blocks + nb rhs rows), then the one-workgroup factor / solve / retraction
 // step_tasks / step_base / step_na: per wide step its tasks, its first task record, its factor tasks (the rest are
 // update groups)
-extern "C" hipError_t m3s_launch_ba_snode(const BaArgs* a, int nwg, hipStream_t s);
 
 // XCD affinity of the solve (M3S_BA_XCD0, default on): every multi-workgroup factor step and the one-workgroup kernel
 // (block 0) run on XCD 0, so each step reads the previous one's blocks from that XCD's L2 instead of across the
@@ -1899,48 +1485,21 @@ extern "C" hipError_t m3s_launch_ba_solve(const BaArgs* a, int K, int nL, float 
   // the assembly stays spread over every XCD: pinned to XCD 0 (32 CUs, item-strided) it took longer than the L2 reads
   // it saved the first step (solve C5 0.381 vs 0.375 ms)
   if (a->nb > 0) hipLaunchKernelGGL(m3s::ba_assemble_kernel, dim3(nL + a->nb), dim3(64), 0, s, *a, nL, 1);
-  if (a->snode) {  // supernodal factor (ba_snode.hip), then the back substitution + retraction on a factor-free schedule
-    const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64 + (size_t)a->nb * 12;
-    if (!a->flow || lds > (size_t)m3s::SP_PLAN_BYTES) return hipErrorInvalidValue;
-    if (a->nb > 0) {
-      const hipError_t e = m3s_launch_ba_snode(a, a->sn_wgs, s);
-      if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
-    return hipGetLastError();
-  }
-  static_assert(m3s::SUB_WAVES == 8, "abi.cpp BA_SUB_WAVES");
-  static_assert(m3s::FRONT_LDS_BYTES == 159 * 1024, "abi.cpp BA_FRONT_LDS_BYTES");
   // LDS: the plan tables, x (8 doubles per column) and, for the dataflow schedule, 3 flags per column
   const size_t lds = ((a->plan_bytes + 15) & ~15) + (size_t)a->nb * 64;
   const bool flow_fits = a->flow && lds + (size_t)a->nb * 12 <= (size_t)m3s::SP_PLAN_BYTES;
-  // the subtree phase leaves the spine-targeted groups of its steps to the dataflow schedule (the plan only builds
-  // one when that schedule fits: a level-synchronous run would re-factor the subtrees' columns)
-  if (a->sub_wgs > 0 && !flow_fits) return hipErrorInvalidValue;
-  if (a->sub_wgs > 0) hipLaunchKernelGGL(m3s::ba_subtree_kernel, dim3(a->sub_wgs), dim3(m3s::SUB_WAVES * 64), 0, s, *a);
-  // the frontal subtree phase: steps [0, front_cut) in LDS, then the U columns into the targets above the cut; the
-  // launched steps resume at front_cut (their records leave out the groups the U columns replaced)
-  if (a->front_wgs > 0) {
-    hipLaunchKernelGGL(m3s::ba_front_kernel, dim3(a->front_wgs), dim3(m3s::FRONT_WAVES * 64), 0, s, *a);
-    if (a->front_napply > 0) hipLaunchKernelGGL(m3s::ba_front_apply_kernel, dim3(a->front_napply), dim3(64), 0, s, *a);
-  }
-  for (int l = a->front_wgs > 0 ? a->front_cut : 0; l < a->wide_steps; l++)
+  for (int l = 0; l < a->wide_steps; l++)
     if (step_tasks[l] > 0)
       hipLaunchKernelGGL(m3s::ba_sparse_step_kernel, dim3(step_tasks[l] * xs), dim3(64), 0, s, *a, step_base[l],
                          step_na[l], xs);
-  if (flow_fits && a->top_T > 0) {  // dense top phase between a factor-only and a back-substitution-only run
-    if (a->top_T > m3s::TOP_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 1);
-    hipLaunchKernelGGL(m3s::ba_dense_top_kernel, dim3(1), dim3(1024), 0, s, *a);
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 2);
-  } else if (flow_fits)
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
+  if (flow_fits)
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   else if (lds <= (size_t)m3s::SP_PLAN_BYTES) {
     BaArgs b = *a;
     b.flow = 0;
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, b, K, nL, delta_thresh, 0);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<true>, dim3(1), dim3(1024), 0, s, b, K, nL, delta_thresh);
   }
   else
-    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh, 0);
+    hipLaunchKernelGGL(m3s::ba_sparse_factor_kernel<false>, dim3(1), dim3(1024), 0, s, *a, K, nL, delta_thresh);
   return hipGetLastError();
 }

@@ -269,7 +269,7 @@ std::vector<int> col_levels(const BaPattern& P) {
     for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) lev[P.lev_col[c]] = l;
   return lev;
 }
-// estimated task costs (us), shared by the flow schedule and the subtree plan: a factor task ~1.5 + its pull
+// estimated task costs (us) of the flow schedule: a factor task ~1.5 + its pull
 // group, an update group ~0.8, ~0.3 per source and 64-row pass (one wave alone on its SIMD issues one fp64
 // instruction per ~3.3 ns)
 inline int col_passes(const BaPattern& P, int j) { return (7 * (P.col_ptr[j + 1] - P.col_ptr[j]) + 1 + 63) / 64; }
@@ -283,141 +283,12 @@ inline double group_cost(const BaPattern& P, int g) {
 }
 }  // namespace
 
-int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vector<int>* tab, double* cost_us) {
-  const int nb = P.nb;
-  tab->clear();
-  *cost_us = 0.0;
-  cut = std::min(cut, P.nlev);
-  if (nb <= 0 || cut <= 0) return 0;
-  const std::vector<int> lev = col_levels(P);
-  // subtree root of every column below the cut (parents have higher indices: one downward pass)
-  std::vector<int> root(nb, -1);
-  for (int j = nb - 1; j >= 0; j--) {
-    if (lev[j] >= cut) continue;
-    const int p = P.col_ptr[j + 1] - P.col_ptr[j] > 1 ? P.rowL[P.col_ptr[j] + 1] : -1;
-    root[j] = (p < 0 || lev[p] >= cut) ? j : root[p];
-  }
-  // per subtree and step: its factor tasks and its groups (targets below the cut)
-  std::vector<int> sid(nb, -1), roots;
-  for (int j = 0; j < nb; j++)
-    if (root[j] == j) {
-      sid[j] = (int)roots.size();
-      roots.push_back(j);
-    }
-  const int ns = (int)roots.size();
-  std::vector<std::vector<std::vector<int>>> fac(ns, std::vector<std::vector<int>>(cut)), grp = fac;
-  for (int l = 0; l < cut; l++) {
-    for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
-      const int j = P.lev_col[c];
-      fac[sid[root[j]]][l].push_back(j);
-    }
-    for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
-      const int j = P.grp[4 * (size_t)t];
-      if (lev[j] < cut) grp[sid[root[j]]][l].push_back(t);
-    }
-  }
-  // per-step cost of a set of tasks on `waves` waves (greedy, longest first) + a barrier
-  auto step_cost = [&](const std::vector<double>& c) {
-    if (c.empty()) return 0.0;
-    std::vector<double> w(waves, 0.0), cs = c;
-    std::sort(cs.rbegin(), cs.rend());
-    for (double x : cs) *std::min_element(w.begin(), w.end()) += x;
-    return *std::max_element(w.begin(), w.end()) + 0.3;
-  };
-  std::vector<double> scost(ns, 0.0);
-  for (int s = 0; s < ns; s++)
-    for (int l = 0; l < cut; l++) {
-      std::vector<double> c;
-      for (int j : fac[s][l]) c.push_back(factor_cost(P, j));
-      for (int t : grp[s][l]) c.push_back(group_cost(P, t));
-      scost[s] += step_cost(c);
-    }
-  // pack subtrees into at most max_wg workgroups: longest first onto the least loaded (their steps merge)
-  const int nwg = std::min(ns, std::max(1, max_wg));
-  std::vector<int> order(ns);
-  for (int s = 0; s < ns; s++) order[s] = s;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return scost[a] > scost[b]; });
-  std::vector<double> load(nwg, 0.0);
-  std::vector<std::vector<int>> members(nwg);
-  for (int s : order) {
-    const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    load[w] += scost[s];
-    members[w].push_back(s);
-  }
-  tab->assign((size_t)nwg * cut * 4, 0);
-  for (int w = 0; w < nwg; w++) {
-    double wc = 0.0;
-    for (int l = 0; l < cut; l++) {
-      int* e = tab->data() + ((size_t)w * cut + l) * 4;
-      const int first = (int)(tab->size() - (size_t)nwg * cut * 4) / 8;
-      int na = 0, nt = 0;
-      std::vector<double> c;
-      auto put = [&](int j, int g) {
-        const int* gq = g >= 0 ? &P.grp[4 * (size_t)g] : nullptr;
-        const int r[8] = {j, P.col_ptr[j], P.col_ptr[j + 1], g, gq ? gq[1] : 0, gq ? gq[2] : 0, 0, 0};
-        tab->insert(tab->end(), r, r + 8);
-        nt++;
-      };
-      for (int s : members[w])
-        for (int j : fac[s][l]) {
-          put(j, P.pull_grp[j]);
-          na++;
-          c.push_back(factor_cost(P, j));
-        }
-      for (int s : members[w])
-        for (int t : grp[s][l]) {
-          put(P.grp[4 * (size_t)t], t);
-          c.push_back(group_cost(P, t));
-        }
-      e = tab->data() + ((size_t)w * cut + l) * 4;  // (the inserts may have moved the table)
-      e[0] = first;
-      e[1] = nt;
-      e[2] = na;
-      wc += step_cost(c);
-    }
-    *cost_us = std::max(*cost_us, wc);
-  }
-  return nwg;
-}
-
-int ba_top_plan(const BaPattern& P, int top, std::vector<int>* tab) {
-  tab->clear();
-  if (top <= 0 || top >= P.nlev) return 0;
-  const std::vector<int> lev = col_levels(P);
-  std::vector<int> cols, pos(P.nb, -1);
-  for (int j = 0; j < P.nb; j++)
-    if (lev[j] >= top) {
-      pos[j] = (int)cols.size();
-      cols.push_back(j);
-    }
-  const int T = (int)cols.size();
-  tab->assign(4 + T + (size_t)T * T, -1);
-  int* t = tab->data();
-  t[0] = T;
-  t[1] = top;
-  t[2] = t[3] = 0;
-  for (int a = 0; a < T; a++) t[4 + a] = cols[a];
-  int* map = t + 4 + T;
-  for (int b = 0; b < T; b++) {
-    const int j = cols[b];
-    for (int q = P.col_ptr[j]; q < P.col_ptr[j + 1]; q++) {
-      const int a = pos[P.rowL[q]];
-      if (a < 0) {  // struct(j) of a top column holds only its ancestors: top columns
-        tab->clear();
-        return 0;
-      }
-      map[(size_t)a * T + b] = q;
-    }
-  }
-  return T;
-}
-
-double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub, int top) {
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched) {
   const int nb = P.nb, nlev = P.nlev;
   sched->clear();
   if (nb <= 0) return 0.0;
   const std::vector<int> lev = col_levels(P);
-  const int done_below = std::max(wide, sub);  // columns factored before the one-workgroup kernel starts
+  const int done_below = std::max(wide, 0);  // columns factored before the one-workgroup kernel starts
   // estimated task costs (factor_cost / group_cost), hand-off ~0.15 us
   FlowSim F(waves, 0.15);
   std::vector<std::pair<int, int>> tasks;  // {code, q}
@@ -428,30 +299,19 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
       if (fac_task[k] >= 0) deps.push_back(fac_task[k]);
     }
   };
-  const bool has_top = top > 0 && top < nlev;
   for (int l = std::max(0, wide); l <= nlev; l++) {
-    if (l < nlev && l >= sub)
+    if (l < nlev)
       for (int c = P.lev_ptr[l]; c < P.lev_ptr[l + 1]; c++) {
         const int j = P.lev_col[c], g = P.pull_grp[j];
         deps.clear();
         if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
         if (g >= 0) src_deps(g);
-        if (has_top && l >= top) {  // the dense top phase factors j; its pull group runs here when its sources do not
-          if (l == top && g >= 0) {
-            last_grp[j] = (int)tasks.size();
-            tasks.push_back({-1 - g, napplied[j]++});
-            F.place(deps, group_cost(P, g));
-          }
-          continue;
-        }
         fac_task[j] = (int)tasks.size();
         tasks.push_back({j, napplied[j]});
         F.place(deps, factor_cost(P, j));
       }
-    if (has_top && l - 1 >= top) continue;  // groups with top sources: the dense phase
     for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
       const int j = P.grp[4 * (size_t)t];
-      if (l < sub && lev[j] < sub) continue;  // a subtree's own group: the subtree launch ran it
       deps.clear();
       if (last_grp[j] >= 0) deps.push_back(last_grp[j]);
       src_deps(t);
@@ -467,7 +327,6 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
   FlowSim B(waves, 0.15);
   std::vector<int> bcol, bwave(nb, -1), btask(nb, -1);
   for (int j = nb - 1; j >= 0; j--) {
-    if (has_top && lev[j] >= top) continue;  // solved by the dense top phase (x and its flag preset)
     deps.clear();
     if (P.col_ptr[j + 1] - P.col_ptr[j] > 1 && btask[P.rowL[P.col_ptr[j] + 1]] >= 0)
       deps.push_back(btask[P.rowL[P.col_ptr[j] + 1]]);
@@ -508,160 +367,3 @@ double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int
   return makespan;
 }
 
-int ba_front_plan(const BaPattern& P, int cut, size_t lds_bytes, std::vector<int>* tab, std::vector<int>* apply,
-                  size_t* u_doubles, int* napply) {
-  const int nb = P.nb;
-  tab->clear();
-  apply->clear();
-  *u_doubles = 0;
-  *napply = 0;
-  cut = std::min(cut, P.nlev);
-  if (nb <= 0 || cut <= 0) return 0;
-  const std::vector<int> lev = col_levels(P);
-  std::vector<int> root(nb, -1);
-  for (int j = nb - 1; j >= 0; j--) {
-    if (lev[j] >= cut) continue;
-    const int p = P.col_ptr[j + 1] - P.col_ptr[j] > 1 ? P.rowL[P.col_ptr[j] + 1] : -1;
-    root[j] = (p < 0 || lev[p] >= cut) ? j : root[p];
-  }
-  std::vector<int> roots, sid(nb, -1);
-  for (int j = 0; j < nb; j++)
-    if (root[j] == j) {
-      sid[j] = (int)roots.size();
-      roots.push_back(j);
-    }
-  const int ns = (int)roots.size();
-  std::vector<std::vector<int>> cols(ns);
-  for (int j = 0; j < nb; j++)
-    if (root[j] >= 0) cols[sid[root[j]]].push_back(j);
-  auto nblk = [&](int j) { return P.col_ptr[j + 1] - P.col_ptr[j]; };
-  std::vector<int> gslot(P.nL, -1), ycol(nb, -1);
-  std::vector<int> slot(nb, -1), stamp(nb, 0);  // block of the current source column at a row (build_pattern's trick)
-  std::vector<std::vector<int>> ulist(nb);      // per target above the cut: U offsets, workgroups ascending
-  std::vector<std::vector<int>> by_tgt(nb);
-  size_t uoff = 0;
-  std::vector<int> dir((size_t)4 * ns, 0), body;
-  for (int s = 0; s < ns; s++) {
-    const std::vector<int>& C = cols[s];
-    std::vector<int> slot_gb, colj, rec, src, sx;
-    for (int j : C) {
-      ycol[j] = (int)colj.size();
-      colj.push_back(j);
-      for (int b = P.col_ptr[j]; b < P.col_ptr[j + 1]; b++) {
-        gslot[b] = (int)slot_gb.size();
-        slot_gb.push_back(b);
-      }
-    }
-    // one translated source: L_jk's slot, k's rhs row, and per block of the target j the slot of column k's block
-    // at that row (-1 where struct(k) misses it)
-    auto put_src = [&](int j, int k) {
-      int bjk = -1;
-      for (int q = P.col_ptr[k] + 1; q < P.col_ptr[k + 1]; q++) {
-        slot[P.rowL[q]] = q;
-        stamp[P.rowL[q]] = k + 1;
-        if (P.rowL[q] == j) bjk = q;
-      }
-      src.push_back(gslot[bjk]);
-      src.push_back(ycol[k]);
-      src.push_back((int)sx.size());
-      src.push_back(0);
-      for (int b = P.col_ptr[j]; b < P.col_ptr[j + 1]; b++) {
-        const int i = P.rowL[b];
-        sx.push_back(stamp[i] == k + 1 ? gslot[slot[i]] : -1);
-      }
-    };
-    auto put_rec = [&](int kind, int j, int s0, int s1, long long u) {
-      const int r[8] = {kind, kind == 2 ? 0 : gslot[P.col_ptr[j]], nblk(j), kind == 2 ? 0 : ycol[j], s0, s1,
-                        (int)u, 0};
-      rec.insert(rec.end(), r, r + 8);
-    };
-    auto grp_sources = [&](int j, int g) {  // an existing group's sources (all inside this subtree), translated
-      const int s0 = (int)src.size() / 4;
-      for (int e = P.grp[4 * (size_t)g + 1]; e < P.grp[4 * (size_t)g + 2]; e++) put_src(j, P.src[4 * (size_t)e + 1]);
-      return s0;
-    };
-    std::vector<int> steps;
-    for (int l = 0; l < cut; l++) {
-      const int first = (int)rec.size() / 8;
-      for (int j : C)
-        if (lev[j] == l) {
-          const int g = P.pull_grp[j];
-          const int s0 = g >= 0 ? grp_sources(j, g) : (int)src.size() / 4;
-          put_rec(0, j, s0, (int)src.size() / 4, 0);
-        }
-      for (int t = P.grp_ptr[l]; t < P.grp_ptr[l + 1]; t++) {
-        const int j = P.grp[4 * (size_t)t];
-        if (lev[j] >= cut || sid[root[j]] != s) continue;
-        const int s0 = grp_sources(j, t);
-        put_rec(1, j, s0, (int)src.size() / 4, 0);
-      }
-      steps.push_back(first);
-      steps.push_back((int)rec.size() / 8 - first);
-    }
-    // U tasks: every target above the cut, its sources (this subtree's columns) ascending
-    std::vector<int> tg;
-    for (int k : C)
-      for (int b = P.col_ptr[k] + 1; b < P.col_ptr[k + 1]; b++) {
-        const int j = P.rowL[b];
-        if (lev[j] < cut) continue;
-        if (by_tgt[j].empty()) tg.push_back(j);
-        by_tgt[j].push_back(k);
-      }
-    std::sort(tg.begin(), tg.end());
-    const int ufirst = (int)rec.size() / 8;
-    for (int j : tg) {
-      const int s0 = (int)src.size() / 4;
-      for (int k : by_tgt[j]) put_src(j, k);
-      by_tgt[j].clear();
-      if (uoff > (size_t)INT32_MAX - 64 * (size_t)P.nL) return 0;
-      put_rec(2, j, s0, (int)src.size() / 4, (long long)uoff);
-      ulist[j].push_back((int)uoff);
-      uoff += (size_t)8 * (7 * nblk(j) + 1);
-    }
-    steps.push_back(ufirst);
-    steps.push_back((int)rec.size() / 8 - ufirst);
-    for (int j : C) ycol[j] = -1;
-    for (int b : slot_gb) gslot[b] = -1;
-    // the table, 16-B aligned sections
-    std::vector<int> t(16, 0);
-    auto sec = [&](const std::vector<int>& v) {
-      const int o = (int)t.size();
-      t.insert(t.end(), v.begin(), v.end());
-      while (t.size() % 4) t.push_back(0);
-      return o;
-    };
-    sec(steps);
-    t[4] = sec(rec);
-    t[5] = sec(src);
-    t[6] = sec(sx);
-    t[7] = sec(slot_gb);
-    t[8] = sec(colj);
-    t[0] = (int)slot_gb.size();
-    t[1] = (int)colj.size();
-    t[2] = cut;
-    const size_t lds = (size_t)slot_gb.size() * 56 * 8 + colj.size() * 64 + t.size() * 4;
-    if (lds > lds_bytes) {
-      tab->clear();
-      return 0;
-    }
-    dir[4 * (size_t)s] = (int)body.size();
-    dir[4 * (size_t)s + 1] = (int)t.size();
-    body.insert(body.end(), t.begin(), t.end());
-  }
-  for (int s = 0; s < ns; s++) dir[4 * (size_t)s] += 4 * ns;
-  tab->assign(dir.begin(), dir.end());
-  tab->insert(tab->end(), body.begin(), body.end());
-  // apply entries (targets ascending) and their U lists
-  std::vector<int> ent, lists;
-  for (int j = 0; j < nb; j++) {
-    if (ulist[j].empty()) continue;
-    const int r[8] = {j, P.col_ptr[j], nblk(j), (int)lists.size(), (int)(lists.size() + ulist[j].size()), 0, 0, 0};
-    ent.insert(ent.end(), r, r + 8);
-    lists.insert(lists.end(), ulist[j].begin(), ulist[j].end());
-  }
-  *napply = (int)ent.size() / 8;
-  apply->assign(ent.begin(), ent.end());
-  apply->insert(apply->end(), lists.begin(), lists.end());
-  *u_doubles = uoff;
-  return ns;
-}

@@ -61,66 +61,5 @@ void ba_build_pattern(const int* ri, const int* rj, int E, int Kp, BaPattern* P,
 // the low 24 bits.
 #define BA_BS_NOWAIT (1 << 30)
 #define BA_BS_COL 0xFFFFFF
-// sub > 0 (subtree phase below, wide = 0): steps [0, sub) belong to the subtree launch except their update groups
-// whose target column sits at level >= sub, which the one-workgroup schedule runs first (in step order per target).
-// top > 0 (dense top phase, ba_top_plan): the columns at levels >= top are factored and solved by ba_dense_top_kernel
-// between a factor-only and a back-substitution-only run of the one-workgroup kernel: their factor tasks, the update
-// groups whose sources sit at levels >= top and their back-substitution tasks leave the lists; the pull groups of the
-// columns at level `top` (sources below the cut) become update-group tasks.
 // Returns the simulated finish time (us) of the factor part (the cost model's estimate).
-double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched, int sub = 0, int top = 0);
-
-// Dense top phase (ba_dense_top_kernel, ba.hip): the columns at elimination-tree levels >= `top` (an ancestor-closed
-// set: the root end of the tree, where the factor is nearly dense) as one dense (7T x 7T) fp64 Cholesky on the matrix
-// cores in one workgroup. Layout (ints): [T, top, 0, 0] [top columns ascending (T)] [T x T: the factor block of
-// L(row top_col[a], column top_col[b]) for a >= b, or -1 where the pattern has none]. Returns T (0: no top phase).
-int ba_top_plan(const BaPattern& P, int top, std::vector<int>* tab);
-
-// Subtree phase (ba_subtree_kernel, ba.hip): the columns below elimination-tree level `cut` fall into independent
-// subtrees (a column belongs to its highest ancestor below the cut). One workgroup per subtree (small subtrees
-// packed together, at most max_wg workgroups) runs steps [0, cut) of its columns level by level: their factor tasks
-// (each with its pull group) and the update groups whose target is one of its columns; a barrier between steps.
-// Every column's groups still apply in step order, with the same per-task arithmetic: the factor is bit-identical to
-// the level-synchronous schedule. Layout (ints): per workgroup `cut` int4 step entries {first record, tasks, factor
-// tasks (first), 0}, then 8-int task records {j, b0, b1, pull group or -1 (factor task) | group, src begin, src end,
-// 0, 0}. Returns the number of workgroups; *cost_us = the estimated finish time of the slowest workgroup.
-int ba_subtree_plan(const BaPattern& P, int cut, int waves, int max_wg, std::vector<int>* tab, double* cost_us);
-
-// Frontal subtree phase (ba_front_kernel / ba_front_apply_kernel, ba.hip): the columns below elimination-tree level
-// `cut` fall into independent subtrees; ONE launch runs one workgroup per subtree with the subtree's factor blocks,
-// rhs rows and translated task tables resident in LDS (global -> LDS once, every step an LDS hand-off behind a
-// workgroup barrier, LDS -> global once). The subtree's contributions to the columns above the cut are not applied as
-// the level's update groups: each workgroup sums them per target column (its sources ascending) into a dense update
-// column U_(W,j) laid out like column j's rows (rhs last) in a scratch region, and a second launch adds the U columns
-// of every target (workgroups ascending) into L / y. The steps [cut, ...) then run without the groups whose sources
-// lie below the cut (every step <= cut; the factor tasks of level `cut` pull nothing). Deterministic (fixed orders),
-// but not bit-identical to the group schedules (the below-cut sums are associated per subtree).
-// Layout of `tab` (ints): per workgroup an int4 {table offset, table ints (multiple of 4), 0, 0}, then the tables:
-//   [16-int header: nslots, ncols, cut, 0, off_rec, off_src, off_sidx, off_slotgb, off_colj, 0...]
-//   [cut + 1 int2 steps {first record, tasks}; entry `cut` = the U tasks]
-//   [records 8 ints: {kind 0 factor | 1 group | 2 U, slot0, nblk, yslot, src begin, src end, U offset, 0}]
-//   [sources int4 {slot of L_jk, yslot of k, sidx offset, 0}] [sidx: per source, per block of the target: slot or -1]
-//   [slot -> global block] [yslot -> column]
-// LDS image per workgroup: nslots blocks of 56 doubles (rows 0..6 of the 8x8 block), ncols rhs rows of 8 doubles,
-// then the table; lds_bytes bounds it. `apply` (ints): napply 8-int entries {j, first block, nblk, list begin, list
-// end, 0, 0, 0} (targets ascending), then the lists of U offsets (doubles into the scratch region). Returns the
-// number of workgroups (0: the cut does not fit); *u_doubles = the scratch size, *napply = the apply entries.
-int ba_front_plan(const BaPattern& P, int cut, size_t lds_bytes, std::vector<int>* tab, std::vector<int>* apply,
-                  size_t* u_doubles, int* napply);
-
-// Supernodal factorisation (ba_snode.hip, ba_snode.cpp): chains of consecutive etree columns as supernodes of at most
-// `smax` columns, each a dense register panel of one group of 4 waves (7 rows per block row + the rhs row, at most
-// `max_rows` rows), left-looking pulls from every descendant column, the supernodal tree cut at a height (cut_req >= 0
-// forces it, -1 picks the estimate's best): the subtrees below in a multi-workgroup launch, the rest in one
-// workgroup; `groups` groups per workgroup walk list-scheduled supernode lists. Layout (ints):
-//   [16-int header: nsn, nwg (bottom workgroups), off_rec, off_pull, off_lists, cut height, groups, smax, max pairs,
-//    tree height]
-//   [records 8 ints per supernode: {s, R, rows offset, blk offset, pull begin, pull end, child begin, child end}]
-//   per supernode: rows (R block rows: its columns, then the rows below), blk (s x R: factor block of L(row ib,
-//   column t) or -1), children, per pull its map (R: block of L(row ib, k) or -1)
-//   [pulls: 2 ints {k, map offset}]
-//   [lists: (nwg + 1) x (groups + 1) item offsets: workgroup w < nwg bottom, w = nwg the top one] [items]
-// Offsets are absolute (ints from the table start). Returns the number of supernodes (0: a panel does not fit or the
-// pattern breaks the row-subset property: use another solver); *cost_us = the estimated makespan.
-int ba_snode_plan(const BaPattern& P, int smax, int groups, int max_rows, int cut_req, std::vector<int>* tab,
-                  int* nwg, double* cost_us);
+double ba_flow_schedule(const BaPattern& P, int wide, int waves, std::vector<int>* sched);

@@ -7,13 +7,6 @@
 #define BA_MODE_RAYS 1
 #define BA_MODE_CALIB 2
 
-#ifndef M3S_BA_SN_GROUPS  // supernodal factorisation (ba_snode.hip): groups of 4 waves per workgroup, columns per supernode
-#define M3S_BA_SN_GROUPS 2
-#endif
-#ifndef M3S_BA_SN_SMAX
-#define M3S_BA_SN_SMAX 4
-#endif
-
 #ifndef M3S_BA_SP_WAVES
 #define M3S_BA_SP_WAVES 16  // waves of the one-workgroup sparse factorisation (ba.hip) and of its cost model (abi.cpp)
 #endif
@@ -76,16 +69,6 @@ struct BaArgs {
   const int* sched;       // dataflow schedule of the one-workgroup part + back substitution (ba_pattern.h)
   int flow;               // sched present (else the level-synchronous loops)
   const int4* step_rec;   // per task of the wide steps, 2 x int4: {j, b0, b1, pull group or -1}, {src begin, end, 0, 0}
-  const int4* sub_tab;    // subtree phase (ba_pattern.h ba_subtree_plan): per workgroup sub_cut step entries, then
-                          // task records (2 x int4, as step_rec)
-  int sub_cut;            // steps [0, sub_cut) run in the subtree launch (0: none)
-  int sub_wgs;            // its workgroups
-  const int* front_tab;   // frontal subtree phase (ba_pattern.h ba_front_plan): per workgroup {table offset, ints}, tables
-  const int* front_apply; // its U columns per target above the cut: 8-int entries, then the U offset lists
-  double* front_u;        // U scratch (doubles; the factor region's tail past the plan's nL blocks)
-  int front_cut;          // steps [0, front_cut) ran in the front launch (0: none)
-  int front_wgs;          // its workgroups
-  int front_napply;       // apply entries
   const char* plan_lo;    // [plan_lo, plan_lo + plan_bytes): col_ptr .. sidx, sched, staged into LDS by the factor kernel
   int plan_bytes;
   const int* asm_ptr;     // (nL+1) assembly CSR: edge*2 + (sign<0), edge order
@@ -102,11 +85,6 @@ struct BaArgs {
   int* done;   // early-exit flag (|dx| < delta_thresh)
   int* iters;  // iterations executed
   int* bad;    // non-positive pivot seen by a multi-workgroup factor step (cleared by the assembly)
-  const int* sn_tab;  // supernodal factorisation (ba_pattern.h ba_snode_plan), or null
-  int snode;          // the factor ran in ba_snode_kernel (the factor kernel then only substitutes back)
-  int sn_wgs;         // its multi-workgroup launch's workgroups
-  const int* top_tab;  // dense top phase (ba_pattern.h ba_top_plan), or null
-  int top_T;           // its poses (0: none)
   int* stalled;  // sticky: a dataflow / LDS hand-off wait timed out in some solve of this plan (M3S_ESTALL)
   int force_stall;  // tests only (M3S_BA_FORCE_STALL): the dataflow waits are never satisfied
 };

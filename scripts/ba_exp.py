@@ -67,8 +67,8 @@ for rep in range(2):
     # edge + 12 B X_j per point and target keyframe + 17 partial / edge-sum rows of 288 B per edge
     gb = (16 * H * W * E + 12 * H * W * info[5] + 17 * 288 * E) / 1e6  # MB -> MB/ms = GB/s
     print(f"rep {rep}: Twc sha1 {twc_hash} E={E} {el / iters * 1e3:.3f} ms/iter  lin {out['ba_linearize']:.3f} ms ({gb / out['ba_linearize']:.0f} GB/s "
-          f"compulsory)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}  wide steps {info[3]}, subtree "
-          f"steps {info[8]} in {info[9]} workgroups, of {info[2]} levels, dense top {info[12]} poses", flush=True)
+          f"compulsory)  solve {out['ba_solve']:.3f} ms  edges/s {E * iters / el:.0f}  wide steps {info[3]} "
+          f"of {info[2]} levels", flush=True)
 
 
 if hasattr(lib, "m3s_debug_sp_stamps"):  # M3S_SP_STAMPS build: phases of the last factor launch

@@ -207,11 +207,9 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
     poses and dx must be bit-identical on the K=256 chess graph:
       * wide elimination-tree steps as multi-workgroup launches (default: the launch-cost model's split;
         M3S_BA_WIDE=t: every step up to the last one wider than t tasks, 0: every step, huge: all steps inside one
-        workgroup), each with the one-workgroup part on its dataflow schedule and level-synchronous (M3S_BA_FLOW=0);
-      * the optional subtree phase (ba_subtree_kernel: one launch, one workgroup per elimination subtree below a cut,
-        the rest in one workgroup) at forced cuts and at its cost model's cut (M3S_BA_SUB=c, 0).
-    The optional frontal phase sums each subtree's contributions above the cut on its own, so it is compared
-    separately (test_ba_k256_front_phase_matches_group_schedules)."""
+        workgroup), each with the one-workgroup part on its dataflow schedule and level-synchronous (M3S_BA_FLOW=0).
+    (Round 5's opt-in subtree / frontal / supernodal / dense-top phases were removed in round 6: git tag
+    ba-solver-experiments-r5.)"""
     import mast3r_slam_backends as B
 
     G = chess_graph
@@ -221,58 +219,23 @@ def test_ba_k256_factor_schedules_bit_identical(chess_graph, monkeypatch):
     args = (c(G["Xs"]), c(G["Cs"]), c(G["ii"]), c(G["jj"]), c(G["idx"]), c(G["valid"], torch.bool), c(G["Q"]))
 
     def run(env):
-        for k in ("M3S_BA_FLOW", "M3S_BA_WIDE", "M3S_BA_SUB"):
+        for k in ("M3S_BA_FLOW", "M3S_BA_WIDE"):
             monkeypatch.delenv(k, raising=False)
-        monkeypatch.setenv("M3S_BA_FRONT", "0")
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         T = c(G["Twc0"])
         dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
         return T.cpu().numpy(), dx.cpu().numpy()
 
-    envs = [{}, {"M3S_BA_SUB": "0"}, {"M3S_BA_SUB": "8"}, {"M3S_BA_SUB": "24"}, {"M3S_BA_SUB": "1"}]
+    envs = [{}]
     for flow in ("1", "0"):
-        envs += [{"M3S_BA_FLOW": flow, "M3S_BA_SUB": "-1"}]
+        envs += [{"M3S_BA_FLOW": flow}]
         envs += [{"M3S_BA_FLOW": flow, "M3S_BA_WIDE": w} for w in ("1000000", "16", "0")]
     ref = run({"M3S_BA_FLOW": "0", "M3S_BA_WIDE": "1000000"})
     for env in envs:
         T, dx = run(env)
         assert np.array_equal(T, ref[0]), f"poses differ with {env}"
         assert np.array_equal(dx, ref[1]), f"dx differs with {env}"
-
-
-def test_ba_k256_front_phase_matches_group_schedules(chess_graph, monkeypatch):
-    """The frontal subtree phase (ba_front_kernel, an option: one launch, each subtree below the cut factored in its
-    workgroup's LDS, its contributions above the cut summed per target into U columns, ba_front_apply_kernel) at the
-    highest cut that fits (M3S_BA_FRONT=-1) and at forced cuts, with the rest on launched steps + the dataflow or
-    level-synchronous one-workgroup kernel: the same solve as the group schedules up to fp64 reassociation of the below-cut sums (deterministic: two
-    runs are bit-identical)."""
-    import mast3r_slam_backends as B
-
-    G = chess_graph
-    sa, sb = SIG["rays"]
-    c = lambda a, dt=None: (torch.from_numpy(np.ascontiguousarray(a)) if dt is None
-                            else torch.from_numpy(np.ascontiguousarray(a)).to(dt)).cuda()
-    args = (c(G["Xs"]), c(G["Cs"]), c(G["ii"]), c(G["jj"]), c(G["idx"]), c(G["valid"], torch.bool), c(G["Q"]))
-
-    def run(env):
-        for k in ("M3S_BA_FLOW", "M3S_BA_WIDE", "M3S_BA_SUB", "M3S_BA_FRONT"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        T = c(G["Twc0"])
-        dx = B.gauss_newton_rays(T, *args, sa, sb, 0.0, 1.5, 10, 1e-8)[0]
-        return T.cpu().numpy(), dx.cpu().numpy()
-
-    ref = run({"M3S_BA_FRONT": "0"})
-    first = run({"M3S_BA_FRONT": "-1"})
-    again = run({"M3S_BA_FRONT": "-1"})
-    assert np.array_equal(first[0], again[0]) and np.array_equal(first[1], again[1])
-    for env in ({"M3S_BA_FRONT": "-1"}, {"M3S_BA_FRONT": "1"}, {"M3S_BA_FRONT": "4"}, {"M3S_BA_FRONT": "12"},
-                {"M3S_BA_FRONT": "8", "M3S_BA_FLOW": "0"}, {"M3S_BA_FRONT": "8", "M3S_BA_WIDE": "2"}):
-        T, dx = run(env)
-        np.testing.assert_allclose(T, ref[0], rtol=0, atol=1e-6, err_msg=str(env))
-        np.testing.assert_allclose(dx, ref[1], rtol=0, atol=1e-6, err_msg=str(env))
 
 
 # The timed BA workloads at their full keyframe resolution (main.py:150-155 solves at the keyframes' own size):
