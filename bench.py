@@ -271,6 +271,22 @@ def roofline(kern, N, gn_iters_mean):
     return out
 
 
+def kernel_table(rl, N, gn_iters_mean):
+    """Per kernel: HIP-event duration, algorithmic bytes and their rate, and beside them the HBM traffic per launch of
+    the newest committed PMC summary (profiles/r??_pmc.json, FETCH_SIZE x2 + WRITE_SIZE) over the same duration, so
+    the two rates can be compared kernel by kernel (gn_iters: per frame, all iterations in one launch)."""
+    alg = {"prep_rays": 192, "proj_occlusion": 77, "refine_lin": 160, "track_setup": 80, "gn_iters": 32 * gn_iters_mean}
+    out = {}
+    for k, v in rl.items():
+        e = pmc_entry(k)
+        t = e["traffic_bytes"] if e else None
+        out[k] = {"avg_us": round(v["avg_us"], 2), "alg_MB": round(alg[k] * N / 1e6, 2), "alg_GBps": round(v["GBps"], 1),
+                  "pmc_MB": round(t / 1e6, 2) if t else None,
+                  "pmc_GBps": round(t / (v["avg_us"] * 1e-6) / 1e9, 1) if t else None,
+                  "pmc_source": e["file"] if e else None}
+    return out
+
+
 KERNEL_SYMBOL = {"prep_rays": "prep_rays_kernel", "proj_occlusion": "proj_occlusion_kernel",
                  "refine_lin": "refine_tile_kernel", "track_setup": "track_setup_kernel", "gn_iters": "gn_loop_kernel"}
 
@@ -607,7 +623,9 @@ def frame_roofline(step_s, N, gn_iters_mean, mode):
     byts = N * (233 + 16 + 29 * it)
     flops = N * (11760 + 1700 + (380 if mode == "calib" else 510) * it)
     t_b, t_f = byts / (HBM_PEAK_GBS * 1e9), flops / (VALU_F32_PEAK_TFLOPS * 1e12)
-    return {"median_ms": med * 1e3, "p90_ms": float(np.percentile(step_s, 90)) * 1e3, "bytes": byts,
+    return {"median_ms": med * 1e3, "p90_ms": float(np.percentile(step_s, 90)) * 1e3,
+            "mean_ms": float(np.mean(step_s)) * 1e3, "max_ms": float(np.max(step_s)) * 1e3,
+            "first_ms": [round(float(x) * 1e3, 4) for x in step_s[:3]], "bytes": byts,
             "flops": flops, "bound": "hbm" if t_b > t_f else "valu", "frac": max(t_b, t_f) / med,
             "note": "host-stamped per-frame wall (track() returns once its result is published), ViT excluded"}
 
@@ -843,6 +861,7 @@ def main():
                                   "backend": dist.get_backend() if world > 1 else None},
                        "gn_iters_mean": gn_iters, "ring_pairs": args.ring},
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rl.items()},
+            "kernels": kernel_table(rl, N, gn_iters),
             "roofline": roof, "frame": frame, "peaks_measured": peaks, "cpu_baseline": cpu, "ba": ba,
             "retrieval": retrieval, "store": store, "configs": configs,
         }

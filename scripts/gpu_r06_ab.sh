@@ -13,15 +13,18 @@ libpath() { if [ "$1" = new ]; then echo lightweight-mast3r-slam_amd/lib/libm3s.
 for L in $LIBS; do
   M3S_LIB=$(libpath $L) timeout -k 10 200 python3 scripts/track_dump.py $OUT/dump_$L.npz > $OUT/dump_$L.log 2>&1
   rc=$?; echo "DUMP_$L=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/dump_$L.log; exit $rc; }
+  M3S_LIB=$(libpath $L) timeout -k 10 200 python3 scripts/match_dump.py $OUT/mdump_$L.npz > $OUT/mdump_$L.log 2>&1
+  rc=$?; echo "MDUMP_$L=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/mdump_$L.log; exit $rc; }
 done
 python3 - "$OUT" $LIBS <<'PY'
 import sys, numpy as np
 out, libs = sys.argv[1], sys.argv[2:]
-ref = np.load(f"{out}/dump_{libs[0]}.npz")
-for L in libs[1:]:
-    d = np.load(f"{out}/dump_{L}.npz")
-    bad = [k for k in ref.files if not np.array_equal(ref[k], d[k], equal_nan=True)]
-    print(f"bit-identical {libs[0]} vs {L}: {not bad} arrays {len(ref.files)} differing {bad[:8]}")
+for pre in ("dump", "mdump"):
+    ref = np.load(f"{out}/{pre}_{libs[0]}.npz")
+    for L in libs[1:]:
+        d = np.load(f"{out}/{pre}_{L}.npz")
+        bad = [k for k in ref.files if not np.array_equal(ref[k], d[k], equal_nan=True)]
+        print(f"{pre} bit-identical {libs[0]} vs {L}: {not bad} arrays {len(ref.files)} differing {bad[:8]}")
 PY
 for r in $(seq 1 $REPS); do
   for L in $LIBS; do
