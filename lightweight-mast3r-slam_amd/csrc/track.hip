@@ -1039,17 +1039,12 @@ __device__ void publish_state(const TrackState* st, TrackPublish pub) {
 // The counting blocks also leave the frame's scratch clean for the next frame on this workspace (the host then
 // skips track_init): the unique-idx byte map (each entry zeroed by the thread that counted it), the setup
 // counters, the GN shard tickets and granules (the publish ticket is re-armed by its last arriver).
-// PPT = 4: four consecutive pixels per thread with 16-B loads and stores (every buffer 16-B aligned and N % 4 == 0,
-// checked by the launcher), the same per-pixel arithmetic in the same order as PPT = 1: bit-identical outputs. One
-// pixel per thread issued ~10 4-B loads per lane; four per thread put every load of the frame in flight at once
-// (a quarter of the blocks).
-template <int PPT>
 __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict__ st, int chunk_id, FuseArgs f,
                                                    int N, uint8_t* __restrict__ flags, int* __restrict__ n_unique,
                                                    TrackPublish pub, int clean_map, unsigned* __restrict__ tick,
                                                    unsigned long long* __restrict__ cnt_words) {
   const bool solved = st->done && st->done_chunk == chunk_id;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * PPT;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x < FUSE_COUNT_BLOCKS) {
     const int tcb = blockIdx.x * 256 + threadIdx.x;  // thread among the counting blocks
     for (int j = tcb; j < M3S_TRACK_TICK_WORDS; j += FUSE_COUNT_BLOCKS * 256)
@@ -1091,58 +1086,19 @@ __global__ void __launch_bounds__(256) fuse_kernel(const TrackState* __restrict_
   float T[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) T[c] = st->T[c];
-  if constexpr (PPT == 1) {
-    const float X[3] = {f.Xkf[3 * (size_t)n], f.Xkf[3 * (size_t)n + 1], f.Xkf[3 * (size_t)n + 2]};
-    float Y[3];
-    actSim3(T, X, Y);
-    const float c0 = f.C_in[n], c1 = f.Ckf[n];
-    const float den = c0 + c1;
-    float Xo[3];
+  const float X[3] = {f.Xkf[3 * (size_t)n], f.Xkf[3 * (size_t)n + 1], f.Xkf[3 * (size_t)n + 2]};
+  float Y[3];
+  actSim3(T, X, Y);
+  const float c0 = f.C_in[n], c1 = f.Ckf[n];
+  const float den = c0 + c1;
+  float Xo[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) Xo[k] = (c0 * f.X_in[3 * (size_t)n + k] + c1 * Y[k]) / den;
+  for (int k = 0; k < 3; k++) Xo[k] = (c0 * f.X_in[3 * (size_t)n + k] + c1 * Y[k]) / den;
 #pragma unroll
-    for (int k = 0; k < 3; k++) f.X_out[3 * (size_t)n + k] = Xo[k];
-    f.C_out[n] = den;
-    if (f.Ck_avg != nullptr) f.Ck_avg[n] = den / f.Nk_new;  // keyframe.get_average_conf()
-    if (f.Cf_avg != nullptr) f.Cf_avg[n] = f.Cf[n] / f.Nf;  // frame.get_average_conf()
-  } else {
-    static_assert(PPT == 4, "fuse: 1 or 4 pixels per thread");
-    // every load first (12 x 16 B), then the math, then the stores (X_out / C_out may alias X_in / C_in: each
-    // thread reads its own pixels before it writes them)
-    float xk[12], xi[12];
-    const float4* pk = reinterpret_cast<const float4*>(f.Xkf + 3 * (size_t)n);
-    const float4* pi = reinterpret_cast<const float4*>(f.X_in + 3 * (size_t)n);
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      const float4 a = pk[q], b = pi[q];
-      xk[4 * q] = a.x, xk[4 * q + 1] = a.y, xk[4 * q + 2] = a.z, xk[4 * q + 3] = a.w;
-      xi[4 * q] = b.x, xi[4 * q + 1] = b.y, xi[4 * q + 2] = b.z, xi[4 * q + 3] = b.w;
-    }
-    const float4 cin = *reinterpret_cast<const float4*>(f.C_in + n);
-    const float4 ckf = *reinterpret_cast<const float4*>(f.Ckf + n);
-    const float4 cf = f.Cf_avg != nullptr ? *reinterpret_cast<const float4*>(f.Cf + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float c0v[4] = {cin.x, cin.y, cin.z, cin.w}, c1v[4] = {ckf.x, ckf.y, ckf.z, ckf.w};
-    const float cfv[4] = {cf.x, cf.y, cf.z, cf.w};
-    float xo[12], den[4], cka[4], cfa[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const float X[3] = {xk[3 * u], xk[3 * u + 1], xk[3 * u + 2]};
-      float Y[3];
-      actSim3(T, X, Y);
-      const float c0 = c0v[u], c1 = c1v[u];
-      den[u] = c0 + c1;
-#pragma unroll
-      for (int k = 0; k < 3; k++) xo[3 * u + k] = (c0 * xi[3 * u + k] + c1 * Y[k]) / den[u];
-      cka[u] = den[u] / f.Nk_new;
-      cfa[u] = cfv[u] / f.Nf;
-    }
-    float4* po = reinterpret_cast<float4*>(f.X_out + 3 * (size_t)n);
-#pragma unroll
-    for (int q = 0; q < 3; q++) po[q] = make_float4(xo[4 * q], xo[4 * q + 1], xo[4 * q + 2], xo[4 * q + 3]);
-    *reinterpret_cast<float4*>(f.C_out + n) = make_float4(den[0], den[1], den[2], den[3]);
-    if (f.Ck_avg != nullptr) *reinterpret_cast<float4*>(f.Ck_avg + n) = make_float4(cka[0], cka[1], cka[2], cka[3]);
-    if (f.Cf_avg != nullptr) *reinterpret_cast<float4*>(f.Cf_avg + n) = make_float4(cfa[0], cfa[1], cfa[2], cfa[3]);
-  }
+  for (int k = 0; k < 3; k++) f.X_out[3 * (size_t)n + k] = Xo[k];
+  f.C_out[n] = den;
+  if (f.Ck_avg != nullptr) f.Ck_avg[n] = den / f.Nk_new;  // keyframe.get_average_conf()
+  if (f.Cf_avg != nullptr) f.Cf_avg[n] = f.Cf[n] / f.Nf;  // frame.get_average_conf()
 }
 
 }  // namespace m3s
@@ -1200,25 +1156,12 @@ extern "C" hipError_t m3s_launch_track_iters(const TrackArgs* a, const TrackPara
 
 // fusion (f->X_in non-null) and/or the unique-match count (count: the state's n_unique from the byte
 // map) for the GN batch chunk_id that finished
-static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
 extern "C" hipError_t m3s_launch_fuse(const TrackArgs* a, int chunk_id, const FuseArgs* f, int count, int N,
                                       const TrackPublish* pub, hipStream_t s) {
-  // four pixels per thread when every fused buffer allows 16-B accesses (the usual case: torch allocations and
-  // keyframe-store rows), else one
-  const bool v4 = f->X_in != nullptr && N % 4 == 0 && al16(f->X_in) && al16(f->C_in) && al16(f->Xkf) && al16(f->Ckf) &&
-                  al16(f->X_out) && al16(f->C_out) && (f->Ck_avg == nullptr || al16(f->Ck_avg)) &&
-                  (f->Cf_avg == nullptr || (f->Cf != nullptr && al16(f->Cf) && al16(f->Cf_avg)));
-  const int ppt = v4 ? 4 : 1;
-  const int need = (N / ppt + 255) / 256;
-  const int grid = need > FUSE_COUNT_BLOCKS ? need : FUSE_COUNT_BLOCKS;  // every counting block publishes
+  const int grid = (N + 255) / 256 > FUSE_COUNT_BLOCKS ? (N + 255) / 256 : FUSE_COUNT_BLOCKS;  // every counting block publishes
   // count: the byte map was written by track_setup (fused path), so it is counted and cleared
-  if (v4)
-    hipLaunchKernelGGL(m3s::fuse_kernel<4>, dim3(grid), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
-                       count ? &a->state->n_unique : nullptr, *pub, count, a->tick, a->cnt);
-  else
-    hipLaunchKernelGGL(m3s::fuse_kernel<1>, dim3(grid), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
-                       count ? &a->state->n_unique : nullptr, *pub, count, a->tick, a->cnt);
+  hipLaunchKernelGGL(m3s::fuse_kernel, dim3(grid), dim3(256), 0, s, a->state, chunk_id, *f, N, a->flags,
+                     count ? &a->state->n_unique : nullptr, *pub, count, a->tick, a->cnt);
   return hipGetLastError();
 }
 

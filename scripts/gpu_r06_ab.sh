@@ -26,6 +26,7 @@ for pre in ("dump", "mdump"):
         bad = [k for k in ref.files if not np.array_equal(ref[k], d[k], equal_nan=True)]
         print(f"{pre} bit-identical {libs[0]} vs {L}: {not bad} arrays {len(ref.files)} differing {bad[:8]}")
 PY
+rm -f $OUT/dump_*.npz $OUT/mdump_*.npz  # ~100 MB: the copy-back limit is 64 MiB
 for r in $(seq 1 $REPS); do
   for L in $LIBS; do
     D=$OUT/prof_${L}_$r
