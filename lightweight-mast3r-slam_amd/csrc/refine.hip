@@ -36,18 +36,37 @@
 
 namespace m3s {
 
+// Tile geometry (RT_WAVES waves per block, two pixel rows per wave). The shipped build: 32 x 8 tiles, 4 waves, a
+// 40-row window (40 KiB, four blocks per CU). RT_TALL (experiment): 32 x 16 tiles, 8 waves, a 56-row window (56 KiB,
+// two blocks per CU: the same 16 waves per CU), so the +-3d halo of a level's window is shared by twice the pixels.
+#ifndef RT_TALL
+#define RT_TALL 0
+#endif
 #define RT_TW 32
-#define RT_TH 8
 #define RT_COLS 64
+#define RT_PCOLS 48
+#if RT_TALL
+#define RT_WAVES 8
+#define RT_TH 16
+#define RT_ROWS 56
+#define RT_PROWS 24
+#define RT_DROWS 36
+#else
+#define RT_WAVES 4
+#define RT_TH 8
 #define RT_ROWS 40  // 40 x 64 x 16 B = 40 KiB per block: four blocks per CU
 // packed window (SCREEN, d = 1): all three chunk planes resident at once, 3 x 17 rows x 48 columns x 16 B = 38.25 KiB
 // (the d = 1 cover is 16 x 39-40 on 97 % of the synthetic 512x512 tiles, scripts/refine_window_stats.py)
-#define RT_PCOLS 48
 #define RT_PROWS 17
-#define RT_PPLANE (RT_PROWS * RT_PCOLS)
 // double-buffered window (SCREEN, d = 2): two 26-row x 48-column chunk buffers (2 x 19.5 KiB), chunk c + 1 streams in
 // while chunk c is screened (the d = 2 cover is 23 x 45-47 on 97.6 % of the synthetic 512x512 tiles)
 #define RT_DROWS 26
+#endif
+static_assert(RT_TH == 2 * RT_WAVES, "two pixel rows per wave");
+static_assert(3 * RT_PROWS * RT_PCOLS <= RT_ROWS * RT_COLS && 2 * RT_DROWS * RT_PCOLS <= RT_ROWS * RT_COLS,
+              "the packed and double-buffered windows share the block's window");
+#define RT_THREADS (64 * RT_WAVES)
+#define RT_PPLANE (RT_PROWS * RT_PCOLS)
 #define RT_DBUF (RT_DROWS * RT_PCOLS)
 #ifndef RT_INPLACE_MAX  // window outliers a wave scores in place at one level (more: deferred to the list)
 #define RT_INPLACE_MAX 8
@@ -307,10 +326,17 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     s_red[wid][3] = mxv;
   }
   __syncthreads();
-  mnu = min(min(s_red[0][0], s_red[1][0]), min(s_red[2][0], s_red[3][0]));
-  mxu = max(max(s_red[0][1], s_red[1][1]), max(s_red[2][1], s_red[3][1]));
-  mnv = min(min(s_red[0][2], s_red[1][2]), min(s_red[2][2], s_red[3][2]));
-  mxv = max(max(s_red[0][3], s_red[1][3]), max(s_red[2][3], s_red[3][3]));
+  mnu = s_red[0][0];
+  mxu = s_red[0][1];
+  mnv = s_red[0][2];
+  mxv = s_red[0][3];
+#pragma unroll
+  for (int w = 1; w < RT_WAVES; w++) {
+    mnu = min(mnu, s_red[w][0]);
+    mxu = max(mxu, s_red[w][1]);
+    mnv = min(mnv, s_red[w][2]);
+    mxv = max(mxv, s_red[w][3]);
+  }
   if (mnu > mxu) {  // no inlier: any window (every active lane is an outlier)
     mnu = mxu = 0;
     mnv = mxv = 0;
@@ -393,7 +419,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     __syncthreads();  // the reduction scratch aliases the window: its readers are done
     if (packed) {  // (d = 1 only) the three chunk planes in one fill
 #ifndef RT_NOLOAD
-      for (int r = wid; r < 3 * nrows; r += 4) {
+      for (int r = wid; r < 3 * nrows; r += RT_WAVES) {
         const int chunk = r >= 2 * nrows ? 2 : (r >= nrows ? 1 : 0), y = r - chunk * nrows;
         const int gy = min(max(wy0 + y, 0), H - 1);
         const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
@@ -415,7 +441,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
     } else if (dbuf) {  // (d = 2 only) chunk c + 1 lands in the other buffer while chunk c is screened
       auto fill = [&](int chunk, int buf) {
 #ifndef RT_NOLOAD
-        for (int y = wid; y < nrows; y += 4) {
+        for (int y = wid; y < nrows; y += RT_WAVES) {
           const int gy = min(max(wy0 + y, 0), H - 1);
           const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
           if (col_in) lds_dma_row(rowp + lane_off, t.lds_addr + (unsigned)(buf + y * RT_PCOLS) * 16u);
@@ -450,7 +476,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
       for (int chunk = 0; chunk < F / 8; chunk++) {
         if (chunk) __syncthreads();
 #ifndef RT_NOLOAD
-        for (int y = wid; y < nrows; y += 4) {
+        for (int y = wid; y < nrows; y += RT_WAVES) {
           const int gy = min(max(wy0 + y, 0), H - 1);
           const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
           if (col_in)
@@ -522,7 +548,7 @@ __device__ __forceinline__ void refine_level(const TileCtx& t, bool& active, con
   for (int chunk = 0; chunk < F / 8; chunk++) {
     if (chunk) __syncthreads();  // previous chunk's readers are done
 #ifndef RT_NOLOAD
-    for (int y = wid; y < nrows; y += 4) {  // one global_load_lds (64 lanes x 16 B) per window row
+    for (int y = wid; y < nrows; y += RT_WAVES) {  // one global_load_lds (64 lanes x 16 B) per window row
       const int gy = min(max(wy0 + y, 0), H - 1);
       const h1* rowp = t.img + (size_t)gy * rstride + chunk * cstride;
       if (col_in) __builtin_amdgcn_global_load_lds((gvoid_t)(rowp + lane_off), (lvoid_t)&lds[y * RT_COLS], 16, 0, 0);
@@ -588,11 +614,11 @@ __device__ __forceinline__ void store_out(void* outv, size_t bn, int W, int cu, 
 // P1_I64: p1 given as (B,N,2) int64 (reference op) else int32 (fused); LIN_OUT: write idx = u + W v.
 // SCREEN: bound-screened scoring (cmaxp = the descriptor-norm bound written by prep / proj_occlusion).
 // LIN_OUT (fused path) reads the PLANAR D11h of prep_rays_kernel.
-#ifndef RT_MIN_BLOCKS  // blocks per CU the register budget is sized for (4: 128 VGPRs, the LDS limit too)
-#define RT_MIN_BLOCKS 4
+#ifndef RT_MIN_BLOCKS  // blocks per CU the register budget is sized for (16 waves: 128 VGPRs, the LDS limit too)
+#define RT_MIN_BLOCKS (16 / RT_WAVES)
 #endif
 template <bool D21_F32, bool P1_I64, bool LIN_OUT, bool SCREEN>
-__global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
+__global__ void __launch_bounds__(RT_THREADS, RT_MIN_BLOCKS) refine_tile_kernel(const h1* __restrict__ D11h, const void* __restrict__ D21,
                                                              const void* __restrict__ p1v, void* __restrict__ outv,
                                                              int H, int W, int dilation_max, int tiles_x,
                                                              int tiles_per_img, int nblocks, int4* olist,
@@ -650,9 +676,16 @@ __global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h
     }
     __syncthreads();
     // block-uniform: SGPRs (readfirstlane), not VGPRs live across every level
-    const int nall = max(1, s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
-    t.fu = __builtin_amdgcn_readfirstlane((s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0]) / nall);
-    t.fv = __builtin_amdgcn_readfirstlane((s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]) / nall);
+    int tu = 0, tv = 0, tn = 0;
+#pragma unroll
+    for (int w = 0; w < RT_WAVES; w++) {
+      tu += s_red[w][0];
+      tv += s_red[w][1];
+      tn += s_red[w][2];
+    }
+    const int nall = max(1, tn);
+    t.fu = __builtin_amdgcn_readfirstlane(tu / nall);
+    t.fv = __builtin_amdgcn_readfirstlane(tv / nall);
     t.tcu = tx * RT_TW + RT_TW / 2 + t.fu;
     t.tcv = ty * RT_TH + RT_TH / 2 + t.fv;
   }
@@ -701,7 +734,9 @@ __global__ void __launch_bounds__(256, RT_MIN_BLOCKS) refine_tile_kernel(const h
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     g_refine_bstamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     g_refine_bstamps[blockIdx.x * 4 + 2] = hw;
-    g_refine_bstamps[blockIdx.x * 4 + 3] = s_act[0] + s_act[1] + s_act[2] + s_act[3];
+    unsigned long long na = 0;
+    for (int w = 0; w < RT_WAVES; w++) na += s_act[w];
+    g_refine_bstamps[blockIdx.x * 4 + 3] = na;
   }
 #endif
 }
@@ -767,14 +802,14 @@ extern "C" hipError_t m3s_launch_refine_tile(const void* D11h, const void* D21, 
   int4* ol = reinterpret_cast<int4*>(olist);
   if (ol == nullptr) ocount = nullptr;
   if (fused && cmax != nullptr)
-    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, true>), dim3(nb), dim3(256), 0, s, a, D21, p1, out,
-                       H, W, dilation_max, tx, tx * ty, nb, ol, ocount, cmax);
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, true>), dim3(nb), dim3(RT_THREADS), 0, s, a, D21, p1,
+                       out, H, W, dilation_max, tx, tx * ty, nb, ol, ocount, cmax);
   else if (fused)
-    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, false>), dim3(nb), dim3(256), 0, s, a, D21, p1, out,
-                       H, W, dilation_max, tx, tx * ty, nb, ol, ocount, nullptr);
-  else
-    hipLaunchKernelGGL((m3s::refine_tile_kernel<false, true, false, false>), dim3(nb), dim3(256), 0, s, a, D21, p1,
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<true, false, true, false>), dim3(nb), dim3(RT_THREADS), 0, s, a, D21, p1,
                        out, H, W, dilation_max, tx, tx * ty, nb, ol, ocount, nullptr);
+  else
+    hipLaunchKernelGGL((m3s::refine_tile_kernel<false, true, false, false>), dim3(nb), dim3(RT_THREADS), 0, s, a, D21,
+                       p1, out, H, W, dilation_max, tx, tx * ty, nb, ol, ocount, nullptr);
   if (ol != nullptr) {
     // 1024 waves: the list is empty or short once waves score up to RT_INPLACE_MAX outliers in place (a smaller
     // grid launches and drains faster); pathological inputs (every lane an outlier) take several passes

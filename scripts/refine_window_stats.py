@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "lightweight-mast3r-slam_amd"))
 from oracle import oracle as O  # noqa: E402  (test infrastructure: the reference restatement)
 from m3s import synthetic  # noqa: E402
 
-TW, TH = 32, 8
+TW, TH = 32, int(os.environ.get("RT_TH", "8"))
 
 
 def main():
