@@ -130,6 +130,33 @@ def gen_matching(H=48, W=64, seed=0):
          idx_init=_np(idx_init), idx_warm=_np(idx_w), valid_warm=_np(valid_w), D11h=_np(D11h).view(np.uint16))
 
 
+# ---------------------------------------------------------------- matching at the config sizes, as digests
+def _digest(a):
+    import hashlib
+
+    a = np.ascontiguousarray(_np(a) if torch.is_tensor(a) else a)
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def gen_match_digest():
+    """The reference's prep_for_iter_proj and match (its torch glue + the oracle's kernels) at the BASELINE config
+    sizes, stored as sha256 digests of the exact bytes (the arrays themselves would be ~10 MB each): C1 512x512
+    (make_pair seed 11, the GPU config tests' pair) and C2 384x512 with the TUM fr1 intrinsics (seed 11)."""
+    out = {}
+    for name, H, W, K in (("C1", 512, 512, None), ("C2", 384, 512, synthetic.tum_fr1_intrinsics(384, 512))):
+        P = synthetic.make_pair(H, W, seed=11, K=K)
+        X, D = P["X"], P["D"]
+        X11, X21, D11, D21 = X[:1], X[1:], D[:1], D[1:]
+        rays, pts, p_init = ref_matching.prep_for_iter_proj(X11, X21, None)
+        idx, valid = ref_matching.match(X11, X21, D11, D21, None)
+        out[f"{name}_shape"] = np.array([H, W])
+        for k, v in (("rays", rays), ("pts", pts), ("idx", idx), ("valid", valid)):
+            out[f"{name}_{k}_sha256"] = np.array(_digest(v))
+        out[f"{name}_rays_row0"] = _np(rays[0, 0])  # a readable slice beside the digest
+        print(name, "valid fraction", float(valid.float().mean()))
+    save("match_digest.npz", **out)
+
+
 # ---------------------------------------------------------------- tracking (opt_pose_* and track())
 class _KFs:
     def __init__(self, kf):
@@ -412,6 +439,7 @@ if __name__ == "__main__":
             globals()["gen_" + name]()
         sys.exit(0)
     gen_matching()
+    gen_match_digest()
     gen_tracking()
     gen_opt_pose()
     gen_ba()

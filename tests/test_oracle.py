@@ -177,3 +177,25 @@ def test_oracle_ba_converges_on_consistent_problem():
                                     np.ones((2, N), np.uint8), np.full((2, N), 2.0, np.float32),
                                     O.ba_params(mode, sa, sb), 10, 1e-8)
         np.testing.assert_allclose(T, Twc_gt, atol=2e-6)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_match_restatement_matches_reference_at_config_size(golden, cfg):
+    """Bit for bit at the BASELINE config sizes (512x512 C1, 384x512 TUM-shaped C2): the reference run's prep
+    (rays, pts) and its full match (its torch glue + the oracle's kernels), stored as sha256 digests by
+    tests/golden/make_golden.py gen_match_digest, against the oracle's restated glue on the same regenerated pair.
+    The GPU config tests then hold the HIP match to the oracle bit for bit on the same pairs."""
+    import hashlib
+
+    from m3s.synthetic import make_pair, tum_fr1_intrinsics
+
+    g = golden("match_digest.npz")
+    H, W = (int(v) for v in g[f"{cfg}_shape"])
+    P = make_pair(H, W, seed=11, K=tum_fr1_intrinsics(H, W) if cfg == "C2" else None)
+    X, D = P["X"].numpy(), P["D"].numpy()
+    rays, pts, _ = O.prep_for_iter_proj(X[:1], X[1:], None)
+    np.testing.assert_array_equal(rays[0, 0], g[f"{cfg}_rays_row0"])
+    idx, valid = O.match(X[:1], X[1:], D[:1], D[1:])
+    dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    for k, v in (("rays", rays), ("pts", pts), ("idx", idx), ("valid", valid)):
+        assert dig(v) == str(g[f"{cfg}_{k}_sha256"]), f"{cfg} {k} differs from the reference run"
