@@ -222,6 +222,49 @@ def gen_tracking(H=48, W=64, seed=3):
          **{f"{t}_{k}": v for t, d in out.items() for k, v in d.items()})
 
 
+def gen_track_config():
+    """The reference's FrameTracker.track (its torch glue, fp32 GN, weighted_pointmap fusion) at the BASELINE config
+    sizes on the GPU config tests' pairs and set-up (tests/test_gpu_configs.py: seed 11, keyframe at the identity,
+    frame starting at the identity): C1 512x512 rays and calib, C2 384x512 calib with the TUM fr1 intrinsics. Stores
+    the frame pose, the GN step count, new_kf and every 997th fused keyframe point (the full pointmap is 3 MB)."""
+    out = {}
+    for name, H, W, calib, K in (("C1_rays", 512, 512, False, None), ("C1_calib", 512, 512, True, None),
+                                 ("C2_calib", 384, 512, True, synthetic.tum_fr1_intrinsics(384, 512))):
+        P = synthetic.make_pair(H, W, seed=11, K=K)
+        X, C, D, Q = P["X"], P["C"], P["D"], P["Q"]
+        N = H * W
+        ref_config.config["use_calib"] = calib
+        kf = _mk_frame(0, H, W)
+        kf.K = P["K"]
+        kf.update_pointmap(P["Xk"], P["Ck"])
+        frame = _mk_frame(1, H, W)
+        tr = ref_tracker.FrameTracker(None, _KFs(kf), "cpu")
+
+        def fake_match(model, frame_i, frame_j, idx_i2j_init=None):
+            idx, valid = ref_matching.match(X[:1], X[1:], D[:1], D[1:], idx_i2j_init)
+            return (idx, valid, X[0].reshape(N, 3), C[0].reshape(N, 1), Q[0].reshape(N, 1), X[1].reshape(N, 3),
+                    C[1].reshape(N, 1), Q[1].reshape(N, 1))
+
+        ref_tracker.mast3r_match_asymmetric = fake_match
+        steps = []
+        orig = ref_tracker.check_convergence
+
+        def counting(*a, **k):
+            steps.append(1)
+            return orig(*a, **k)
+
+        ref_tracker.check_convergence = counting
+        new_kf, info, reloc = tr.track(frame)
+        ref_tracker.check_convergence = orig
+        sub = np.arange(0, N, 997)
+        out.update({f"{name}_T_WCf": _np(frame.T_WC.data), f"{name}_iters": np.array(len(steps)),
+                    f"{name}_new_kf": np.array(new_kf), f"{name}_reloc": np.array(reloc), f"{name}_sub": sub,
+                    f"{name}_kf_X_sub": _np(kf.X_canon)[sub], f"{name}_shape": np.array([H, W])})
+        print(name, "iters", len(steps), "new_kf", new_kf, "T", _np(frame.T_WC.data))
+    ref_config.config["use_calib"] = False
+    save("track_config.npz", **out)
+
+
 def gen_opt_pose(H=32, W=48, seed=5):
     """opt_pose_* on pre-gathered inputs, fixed seeds (tracker.py:173-266)."""
     P = synthetic.make_pair(H, W, seed=seed)
@@ -441,6 +484,7 @@ if __name__ == "__main__":
     gen_matching()
     gen_match_digest()
     gen_tracking()
+    gen_track_config()
     gen_opt_pose()
     gen_ba()
     gen_ba_rows()

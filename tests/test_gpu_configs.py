@@ -17,39 +17,15 @@ import pytest
 import torch
 
 import oracle.oracle as O
+from track_chain import oracle_track as _oracle_track
 
 pytestmark = pytest.mark.gpu
-
-I8 = np.array([0, 0, 0, 0, 0, 0, 1, 1.0])
 
 
 def _pair(H, W, seed, K=None):
     from m3s.synthetic import make_pair
 
     return make_pair(H, W, seed=seed, K=K)
-
-
-def _oracle_track(P, mode, H, W):
-    """tracker.py:28-114 on the oracle: match, Qk, valid_opt, opt_pose_* (fp64), keyframe fusion."""
-    X, C, D, Q = (P[k].numpy() for k in ("X", "C", "D", "Q"))
-    Xk, Ck, K = P["Xk"].numpy(), P["Ck"].numpy()[:, 0], P["K"].numpy()
-    idx, valid = O.match(X[:1], X[1:], D[:1], D[1:])
-    i, vm = idx[0], valid[0, :, 0]
-    Qk = np.sqrt(Q[0].reshape(-1)[i] * Q[1].reshape(-1))
-    v = vm & (C[0].reshape(-1)[i] > 0.0) & (Ck > 0.0) & (Qk > 1.5)
-    if mode == "rays":
-        Tf, Tr, it = O.track_rays(X[0].reshape(-1, 3)[i], Xk, I8, I8, Qk, v)
-    else:
-        Xf = O.backproject_constrain(X[0].reshape(1, -1, 3), K, (H, W))[0][i]
-        z = O.backproject_constrain(Xk[None], K, (H, W))[0][:, 2]
-        u, vv = np.meshgrid(np.arange(W, dtype=np.float32), np.arange(H, dtype=np.float32), indexing="xy")
-        vmk = z > 1e-6
-        meas = np.stack((u.reshape(-1), vv.reshape(-1), np.log(np.where(vmk, z, 1.0))), -1) * vmk[:, None]
-        Tf, Tr, it = O.track_calib(Xf, Xk, I8, I8, Qk, v, meas, vmk, K, (H, W))
-    Xkk = O.sim3_act(Tr, X[1].reshape(-1, 3).astype(np.float64))
-    Ckf = C[1].reshape(-1, 1).astype(np.float64)
-    kX = (Ck[:, None] * Xk + Ckf * Xkk) / (Ck[:, None] + Ckf)
-    return idx, valid, Tf, kX, it
 
 
 def _gpu_track(P, mode, H, W):
@@ -86,7 +62,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("cfg,H,W,mode,K", CASES, ids=[f"{c[0]}-{c[1]}x{c[2]}-{c[3]}" for c in CASES])
-def test_track_at_config_size_matches_oracle(cfg, H, W, mode, K):
+def test_track_at_config_size_matches_oracle(golden, cfg, H, W, mode, K):
     from m3s.synthetic import tum_fr1_intrinsics
 
     P = _pair(H, W, seed=11, K=tum_fr1_intrinsics(H, W) if K == "tum" else None)
@@ -101,6 +77,15 @@ def test_track_at_config_size_matches_oracle(cfg, H, W, mode, K):
     assert g_it == r_it
     np.testing.assert_allclose(g_T, r_T, atol=1e-5)
     np.testing.assert_allclose(g_kX, r_kX, atol=1e-5, rtol=1e-5)
+    # and against the reference's own FrameTracker.track run on the same pair (tests/golden/track_config.npz)
+    ref = golden("track_config.npz")
+    key = f"{cfg}_{mode}"
+    sub = ref[f"{key}_sub"]
+    print(f"{key}: pose err vs the reference run {np.abs(g_T - ref[f'{key}_T_WCf'][0]).max():.2e}, "
+          f"kf X err {np.abs(g_kX.reshape(-1, 3)[sub] - ref[f'{key}_kf_X_sub']).max():.2e}")
+    assert g_it == int(ref[f"{key}_iters"])
+    np.testing.assert_allclose(g_T, ref[f"{key}_T_WCf"][0], atol=1e-5)
+    np.testing.assert_allclose(g_kX.reshape(-1, 3)[sub], ref[f"{key}_kf_X_sub"], atol=1e-5, rtol=1e-5)
 
 
 def test_match_warm_start_at_c1_matches_oracle():

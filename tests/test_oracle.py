@@ -199,3 +199,24 @@ def test_match_restatement_matches_reference_at_config_size(golden, cfg):
     dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     for k, v in (("rays", rays), ("pts", pts), ("idx", idx), ("valid", valid)):
         assert dig(v) == str(g[f"{cfg}_{k}_sha256"]), f"{cfg} {k} differs from the reference run"
+
+
+@pytest.mark.parametrize("case", ["C1_rays", "C1_calib", "C2_calib"])
+def test_track_restatement_matches_reference_at_config_size(golden, case):
+    """The oracle's tracker chain (tests/track_chain.py: O.match, fp64 opt_pose_*, weighted_pointmap fusion) against
+    the reference's own FrameTracker.track run at the config sizes (tests/golden/make_golden.py gen_track_config:
+    its torch glue and fp32 GN on the same pair): the same GN step count and new_kf decision, the frame pose within
+    the 1e-5 contract, the fused keyframe points (every 997th) within 1e-5 absolute + relative."""
+    from m3s.synthetic import make_pair, tum_fr1_intrinsics
+    from track_chain import oracle_track
+
+    g = golden("track_config.npz")
+    H, W = (int(v) for v in g[f"{case}_shape"])
+    mode = "rays" if case.endswith("rays") else "calib"
+    P = make_pair(H, W, seed=11, K=tum_fr1_intrinsics(H, W) if case.startswith("C2") else None)
+    _, _, Tf, kX, it = oracle_track(P, mode, H, W)
+    print(f"{case}: pose err vs the reference run {np.abs(Tf - g[f'{case}_T_WCf'][0]).max():.2e}, "
+          f"kf X err {np.abs(kX[g[f'{case}_sub']] - g[f'{case}_kf_X_sub']).max():.2e}, iters {it} / {g[f'{case}_iters']}")
+    assert it == int(g[f"{case}_iters"])
+    np.testing.assert_allclose(Tf, g[f"{case}_T_WCf"][0], atol=1e-5)
+    np.testing.assert_allclose(kX[g[f"{case}_sub"]], g[f"{case}_kf_X_sub"], atol=1e-5, rtol=1e-5)
