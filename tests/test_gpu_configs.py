@@ -272,3 +272,22 @@ def test_ba_k256_full_resolution_vs_fp64_truth(case, traj, H, W, mode):
     assert dx.shape == (255, 7)
     np.testing.assert_allclose(T, T_ref, rtol=0, atol=1e-5)
     np.testing.assert_allclose(dx, dx_ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_match_at_config_size_equals_reference_run(golden, cfg):
+    """The fused HIP match against the reference's own prep + match run on the same pair, bit for bit (sha256 of the
+    exact idx / valid bytes, tests/golden/match_digest.npz)."""
+    import hashlib
+
+    from m3s.matching import match
+    from m3s.synthetic import make_pair, tum_fr1_intrinsics
+
+    g = golden("match_digest.npz")
+    H, W = (int(v) for v in g[f"{cfg}_shape"])
+    P = make_pair(H, W, seed=11, K=tum_fr1_intrinsics(H, W) if cfg == "C2" else None)
+    X, D = P["X"].cuda(), P["D"].cuda()
+    idx, valid = match(X[:1], X[1:], D[:1], D[1:])
+    dig = lambda t: hashlib.sha256(np.ascontiguousarray(t.cpu().numpy()).tobytes()).hexdigest()
+    assert dig(idx) == str(g[f"{cfg}_idx_sha256"]), f"{cfg}: idx differs from the reference run"
+    assert dig(valid) == str(g[f"{cfg}_valid_sha256"]), f"{cfg}: valid differs from the reference run"
