@@ -97,6 +97,28 @@ def make_pair(H=64, W=64, Fd=24, seed=0, flow=(3.3, -2.7), rot_deg=1.0, noise=0.
                 T_gt=T_gt, flow=(u1, v1))
 
 
+def make_warm_batch(H, W, seeds, K=None):
+    """A batch of pairs (one per seed) with a warm-start idx_1_to_2_init like a tracker's previous matches
+    (matching.py:25-49 prep's idx path): a shifted identity, with some entries out of range on both sides so that
+    lin_to_pixel's floor semantics and the clamp are exercised. Returns X11, X21 (B,H,W,3), D11, D21 (B,H,W,F),
+    idx_init (B,H*W) int64 (CPU tensors)."""
+    P = [make_pair(H, W, seed=s, K=K) for s in seeds]
+    X11 = torch.stack([p["X"][0] for p in P])
+    X21 = torch.stack([p["X"][1] for p in P])
+    D11 = torch.stack([p["D"][0] for p in P])
+    D21 = torch.stack([p["D"][1] for p in P])
+    vv, uu = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    idx = []
+    for b in range(len(seeds)):
+        u = (uu - 3 + b).clamp(0, W - 1)
+        v = (vv + 2 - b).clamp(0, H - 1)
+        i = (v * W + u).reshape(-1).to(torch.int64)
+        i[::997] = -5 - b  # before the image: v = -1 -> clamped to row 1
+        i[1::991] = H * W + 7 + b  # past the image: v = H -> clamped to row H - 2
+        idx.append(i)
+    return X11, X21, D11, D21, torch.stack(idx)
+
+
 class SyntheticModel:
     """Stands in for MASt3R's asymmetric decoder: returns a ring of resident synthetic outputs."""
 

@@ -154,6 +154,17 @@ def gen_match_digest():
             out[f"{name}_{k}_sha256"] = np.array(_digest(v))
         out[f"{name}_rays_row0"] = _np(rays[0, 0])  # a readable slice beside the digest
         print(name, "valid fraction", float(valid.float().mean()))
+    # C3w: a batch of two TUM-shaped 384x512 pairs (seeds 21, 22) matched from a warm start (synthetic.make_warm_batch:
+    # a shifted identity with out-of-range entries), the batched call global_opt's loop-closure matching makes
+    H, W = 384, 512
+    X11, X21, D11, D21, init = synthetic.make_warm_batch(H, W, (21, 22), K=synthetic.tum_fr1_intrinsics(H, W))
+    rays, pts, p_init = ref_matching.prep_for_iter_proj(X11, X21, init)
+    idx, valid = ref_matching.match(X11, X21, D11, D21, init)
+    out["C3w_shape"] = np.array([H, W])
+    for k, v in (("rays", rays), ("pts", pts), ("p_init", p_init), ("idx", idx), ("valid", valid)):
+        out[f"C3w_{k}_sha256"] = np.array(_digest(v))
+    out["C3w_rays_row0"] = _np(rays[0, 0])
+    print("C3w valid fraction", float(valid.float().mean()))
     save("match_digest.npz", **out)
 
 

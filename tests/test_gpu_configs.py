@@ -291,3 +291,21 @@ def test_match_at_config_size_equals_reference_run(golden, cfg):
     dig = lambda t: hashlib.sha256(np.ascontiguousarray(t.cpu().numpy()).tobytes()).hexdigest()
     assert dig(idx) == str(g[f"{cfg}_idx_sha256"]), f"{cfg}: idx differs from the reference run"
     assert dig(valid) == str(g[f"{cfg}_valid_sha256"]), f"{cfg}: valid differs from the reference run"
+
+
+def test_batched_warm_match_equals_reference_run(golden):
+    """C3w: the fused HIP match on a batch of two 384x512 TUM-shaped pairs from a warm start with out-of-range
+    entries (synthetic.make_warm_batch) against the reference's own prep + match run, bit for bit (sha256 of the
+    idx / valid bytes, tests/golden/match_digest.npz)."""
+    import hashlib
+
+    from m3s.matching import match
+    from m3s.synthetic import make_warm_batch, tum_fr1_intrinsics
+
+    g = golden("match_digest.npz")
+    H, W = (int(v) for v in g["C3w_shape"])
+    X11, X21, D11, D21, init = (t.cuda() for t in make_warm_batch(H, W, (21, 22), K=tum_fr1_intrinsics(H, W)))
+    idx, valid = match(X11, X21, D11, D21, init)
+    dig = lambda t: hashlib.sha256(np.ascontiguousarray(t.cpu().numpy()).tobytes()).hexdigest()
+    assert dig(idx) == str(g["C3w_idx_sha256"]), "C3w: idx differs from the reference run"
+    assert dig(valid) == str(g["C3w_valid_sha256"]), "C3w: valid differs from the reference run"

@@ -201,6 +201,25 @@ def test_match_restatement_matches_reference_at_config_size(golden, cfg):
         assert dig(v) == str(g[f"{cfg}_{k}_sha256"]), f"{cfg} {k} differs from the reference run"
 
 
+def test_batched_warm_match_restatement_matches_reference(golden):
+    """C3w: a batch of two TUM-shaped 384x512 pairs matched from a warm start with out-of-range entries
+    (synthetic.make_warm_batch), the batched call of global_opt's loop-closure matching: the oracle's prep (rays,
+    pts, p_init from idx_init) and match equal the reference run's bytes (gen_match_digest's C3w digests)."""
+    import hashlib
+
+    from m3s.synthetic import make_warm_batch, tum_fr1_intrinsics
+
+    g = golden("match_digest.npz")
+    H, W = (int(v) for v in g["C3w_shape"])
+    X11, X21, D11, D21, init = (t.numpy() for t in make_warm_batch(H, W, (21, 22), K=tum_fr1_intrinsics(H, W)))
+    rays, pts, p_init = O.prep_for_iter_proj(X11, X21, init)
+    np.testing.assert_array_equal(rays[0, 0], g["C3w_rays_row0"])
+    idx, valid = O.match(X11, X21, D11, D21, init)
+    dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    for k, v in (("rays", rays), ("pts", pts), ("p_init", p_init), ("idx", idx), ("valid", valid)):
+        assert dig(v) == str(g[f"C3w_{k}_sha256"]), f"C3w {k} differs from the reference run"
+
+
 @pytest.mark.parametrize("case", ["C1_rays", "C1_calib", "C2_calib"])
 def test_track_restatement_matches_reference_at_config_size(golden, case):
     """The oracle's tracker chain (tests/track_chain.py: O.match, fp64 opt_pose_*, weighted_pointmap fusion) against
