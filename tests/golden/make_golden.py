@@ -276,6 +276,58 @@ def gen_track_config():
     save("track_config.npz", **out)
 
 
+def gen_track_seq():
+    """Three frames tracked in sequence by the reference's own FrameTracker.track against one keyframe, the bench's
+    headline workload (bench.py bench_tracking): 512x512 calib, the bench's synthetic pairs (seeds 0, 1, 2), the
+    keyframe at the identity from pair 0, each frame starting at the previous frame's pose, the tracker's own
+    idx_f2k warm start from frame to frame and weighted_pointmap fusion accumulating in the keyframe (N = 1 -> 4).
+    Stores every frame's pose, GN step count and new_kf, and the final keyframe's N, points and confidences (every
+    997th)."""
+    H, W = 512, 512
+    pairs = [synthetic.make_pair(H, W, seed=s) for s in (0, 1, 2)]
+    N = H * W
+    ref_config.config["use_calib"] = True
+    kf = _mk_frame(0, H, W)
+    kf.K = pairs[0]["K"]
+    kf.update_pointmap(pairs[0]["Xk"], pairs[0]["Ck"])
+    tr = ref_tracker.FrameTracker(None, _KFs(kf), "cpu")
+    cur = {"P": None}
+
+    def fake_match(model, frame_i, frame_j, idx_i2j_init=None):
+        X, C, D, Q = (cur["P"][k] for k in ("X", "C", "D", "Q"))
+        idx, valid = ref_matching.match(X[:1], X[1:], D[:1], D[1:], idx_i2j_init)
+        return (idx, valid, X[0].reshape(N, 3), C[0].reshape(N, 1), Q[0].reshape(N, 1), X[1].reshape(N, 3),
+                C[1].reshape(N, 1), Q[1].reshape(N, 1))
+
+    ref_tracker.mast3r_match_asymmetric = fake_match
+    orig = ref_tracker.check_convergence
+    out = {"S1_shape": np.array([H, W]), "S1_seeds": np.array([0, 1, 2])}
+    T = kf.T_WC
+    for k, P in enumerate(pairs):
+        cur["P"] = P
+        steps = []
+
+        def counting(*a, **kw):
+            steps.append(1)
+            return orig(*a, **kw)
+
+        ref_tracker.check_convergence = counting
+        frame = _mk_frame(k + 1, H, W, T)
+        new_kf, info, reloc = tr.track(frame)
+        ref_tracker.check_convergence = orig
+        assert not reloc, "sequence frame lost"
+        T = frame.T_WC
+        out[f"S1_f{k}_T_WCf"] = _np(T.data)
+        out[f"S1_f{k}_iters"] = np.array(len(steps))
+        out[f"S1_f{k}_new_kf"] = np.array(new_kf)
+        print("S1 frame", k, "iters", len(steps), "new_kf", new_kf, "T", _np(T.data))
+    sub = np.arange(0, N, 997)
+    out.update({"S1_sub": sub, "S1_kf_X_sub": _np(kf.X_canon)[sub], "S1_kf_C_sub": _np(kf.C)[sub],
+                "S1_kf_N": np.array(kf.N)})
+    ref_config.config["use_calib"] = False
+    save("track_seq.npz", **out)
+
+
 def gen_opt_pose(H=32, W=48, seed=5):
     """opt_pose_* on pre-gathered inputs, fixed seeds (tracker.py:173-266)."""
     P = synthetic.make_pair(H, W, seed=seed)
@@ -496,6 +548,7 @@ if __name__ == "__main__":
     gen_match_digest()
     gen_tracking()
     gen_track_config()
+    gen_track_seq()
     gen_opt_pose()
     gen_ba()
     gen_ba_rows()

@@ -309,3 +309,51 @@ def test_batched_warm_match_equals_reference_run(golden):
     dig = lambda t: hashlib.sha256(np.ascontiguousarray(t.cpu().numpy()).tobytes()).hexdigest()
     assert dig(idx) == str(g["C3w_idx_sha256"]), "C3w: idx differs from the reference run"
     assert dig(valid) == str(g["C3w_valid_sha256"]), "C3w: valid differs from the reference run"
+
+
+def test_track_sequence_matches_reference_run(golden):
+    """S1: the HIP FrameTracker over three frames at the bench's headline workload (512x512 calib, the bench's pairs,
+    idx_f2k warm start, each frame from the previous pose, in-device weighted_pointmap fusion) against the reference's
+    own FrameTracker.track run (tests/golden/track_seq.npz): the same GN step counts and new_kf decisions, every pose
+    within the 1e-5 contract, the fused keyframe (every 997th point) within 1e-5 absolute + relative, N equal."""
+    from m3s.config import config
+    from m3s.frame import Frame, Keyframes
+    from m3s.sim3 import Sim3
+    from m3s.synthetic import SyntheticModel, make_pair
+    from m3s.tracker import FrameTracker
+
+    g = golden("track_seq.npz")
+    H, W = (int(v) for v in g["S1_shape"])
+    dev = torch.device("cuda")
+    pairs = [make_pair(H, W, seed=int(s)) for s in g["S1_seeds"]]
+    saved = config["use_calib"]
+    config["use_calib"] = True
+    try:
+        kf = Frame(0, (H, W), T_WC=Sim3.Identity(1, device=dev))
+        kf.K = pairs[0]["K"].to(dev)
+        kf.update_pointmap(pairs[0]["Xk"].to(dev), pairs[0]["Ck"].to(dev))
+        kfs = Keyframes()
+        kfs.append(kf)
+        tr = FrameTracker(SyntheticModel(pairs, dev), kfs, dev)
+        T = kf.T_WC
+        for k in range(len(pairs)):
+            fr = Frame(k + 1, (H, W), T_WC=T)
+            new_kf, _, reloc = tr.track(fr)
+            assert not reloc
+            T = fr.T_WC
+            Tf = T.data.reshape(-1).cpu().numpy()
+            print(f"S1 frame {k}: pose err vs the reference run {np.abs(Tf - g[f'S1_f{k}_T_WCf'][0]).max():.2e}, "
+                  f"iters {tr.last_result.iters} / {int(g[f'S1_f{k}_iters'])}")
+            assert tr.last_result.iters == int(g[f"S1_f{k}_iters"])
+            assert new_kf == bool(g[f"S1_f{k}_new_kf"])
+            np.testing.assert_allclose(Tf, g[f"S1_f{k}_T_WCf"][0], atol=1e-5)
+        kfin = kfs[0]
+        sub = torch.from_numpy(g["S1_sub"]).to(dev)
+        assert kfin.N == int(g["S1_kf_N"])
+        kX = kfin.X_canon[sub].cpu().numpy()
+        kC = kfin.C[sub].cpu().numpy()
+        print(f"S1 keyframe: X err {np.abs(kX - g['S1_kf_X_sub']).max():.2e}, C err {np.abs(kC - g['S1_kf_C_sub']).max():.2e}")
+        np.testing.assert_allclose(kX, g["S1_kf_X_sub"], atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(kC, g["S1_kf_C_sub"], rtol=1e-6)
+    finally:
+        config["use_calib"] = saved
