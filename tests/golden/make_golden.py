@@ -278,19 +278,14 @@ def gen_track_config():
 
 def gen_track_seq():
     """Three frames tracked in sequence by the reference's own FrameTracker.track against one keyframe, the bench's
-    headline workload (bench.py bench_tracking): 512x512 calib, the bench's synthetic pairs (seeds 0, 1, 2), the
-    keyframe at the identity from pair 0, each frame starting at the previous frame's pose, the tracker's own
-    idx_f2k warm start from frame to frame and weighted_pointmap fusion accumulating in the keyframe (N = 1 -> 4).
-    Stores every frame's pose, GN step count and new_kf, and the final keyframe's N, points and confidences (every
-    997th)."""
+    workload (bench.py bench_tracking): 512x512, the bench's synthetic pairs (seeds 0, 1, 2), the keyframe at the
+    identity from pair 0, each frame starting at the previous frame's pose, the tracker's own idx_f2k warm start
+    from frame to frame and weighted_pointmap fusion accumulating in the keyframe (N = 1 -> 4). S1 calib (the
+    headline mode), S2 rays. Stores every frame's pose, GN step count and new_kf, and the final keyframe's N,
+    points and confidences (every 997th)."""
     H, W = 512, 512
     pairs = [synthetic.make_pair(H, W, seed=s) for s in (0, 1, 2)]
     N = H * W
-    ref_config.config["use_calib"] = True
-    kf = _mk_frame(0, H, W)
-    kf.K = pairs[0]["K"]
-    kf.update_pointmap(pairs[0]["Xk"], pairs[0]["Ck"])
-    tr = ref_tracker.FrameTracker(None, _KFs(kf), "cpu")
     cur = {"P": None}
 
     def fake_match(model, frame_i, frame_j, idx_i2j_init=None):
@@ -301,29 +296,37 @@ def gen_track_seq():
 
     ref_tracker.mast3r_match_asymmetric = fake_match
     orig = ref_tracker.check_convergence
-    out = {"S1_shape": np.array([H, W]), "S1_seeds": np.array([0, 1, 2])}
-    T = kf.T_WC
-    for k, P in enumerate(pairs):
-        cur["P"] = P
-        steps = []
+    out = {}
+    for case, calib in (("S1", True), ("S2", False)):
+        ref_config.config["use_calib"] = calib
+        kf = _mk_frame(0, H, W)
+        kf.K = pairs[0]["K"]
+        kf.update_pointmap(pairs[0]["Xk"], pairs[0]["Ck"])
+        tr = ref_tracker.FrameTracker(None, _KFs(kf), "cpu")
+        out.update({f"{case}_shape": np.array([H, W]), f"{case}_seeds": np.array([0, 1, 2]),
+                    f"{case}_calib": np.array(calib)})
+        T = kf.T_WC
+        for k, P in enumerate(pairs):
+            cur["P"] = P
+            steps = []
 
-        def counting(*a, **kw):
-            steps.append(1)
-            return orig(*a, **kw)
+            def counting(*a, **kw):
+                steps.append(1)
+                return orig(*a, **kw)
 
-        ref_tracker.check_convergence = counting
-        frame = _mk_frame(k + 1, H, W, T)
-        new_kf, info, reloc = tr.track(frame)
-        ref_tracker.check_convergence = orig
-        assert not reloc, "sequence frame lost"
-        T = frame.T_WC
-        out[f"S1_f{k}_T_WCf"] = _np(T.data)
-        out[f"S1_f{k}_iters"] = np.array(len(steps))
-        out[f"S1_f{k}_new_kf"] = np.array(new_kf)
-        print("S1 frame", k, "iters", len(steps), "new_kf", new_kf, "T", _np(T.data))
-    sub = np.arange(0, N, 997)
-    out.update({"S1_sub": sub, "S1_kf_X_sub": _np(kf.X_canon)[sub], "S1_kf_C_sub": _np(kf.C)[sub],
-                "S1_kf_N": np.array(kf.N)})
+            ref_tracker.check_convergence = counting
+            frame = _mk_frame(k + 1, H, W, T)
+            new_kf, info, reloc = tr.track(frame)
+            ref_tracker.check_convergence = orig
+            assert not reloc, "sequence frame lost"
+            T = frame.T_WC
+            out[f"{case}_f{k}_T_WCf"] = _np(T.data)
+            out[f"{case}_f{k}_iters"] = np.array(len(steps))
+            out[f"{case}_f{k}_new_kf"] = np.array(new_kf)
+            print(case, "frame", k, "iters", len(steps), "new_kf", new_kf, "T", _np(T.data))
+        sub = np.arange(0, N, 997)
+        out.update({f"{case}_sub": sub, f"{case}_kf_X_sub": _np(kf.X_canon)[sub],
+                    f"{case}_kf_C_sub": _np(kf.C)[sub], f"{case}_kf_N": np.array(kf.N)})
     ref_config.config["use_calib"] = False
     save("track_seq.npz", **out)
 

@@ -311,11 +311,13 @@ def test_batched_warm_match_equals_reference_run(golden):
     assert dig(valid) == str(g["C3w_valid_sha256"]), "C3w: valid differs from the reference run"
 
 
-def test_track_sequence_matches_reference_run(golden):
-    """S1: the HIP FrameTracker over three frames at the bench's headline workload (512x512 calib, the bench's pairs,
-    idx_f2k warm start, each frame from the previous pose, in-device weighted_pointmap fusion) against the reference's
-    own FrameTracker.track run (tests/golden/track_seq.npz): the same GN step counts and new_kf decisions, every pose
-    within the 1e-5 contract, the fused keyframe (every 997th point) within 1e-5 absolute + relative, N equal."""
+@pytest.mark.parametrize("case", ["S1", "S2"])
+def test_track_sequence_matches_reference_run(golden, case):
+    """The HIP FrameTracker over three frames at the bench's workload (512x512, the bench's pairs, idx_f2k warm
+    start, each frame from the previous pose, in-device weighted_pointmap fusion); S1 calib (the headline mode), S2
+    rays. Against the reference's own FrameTracker.track run (tests/golden/track_seq.npz): the same GN step counts
+    and new_kf decisions, every pose within the 1e-5 contract, the fused keyframe (every 997th point) within 1e-5
+    absolute + relative, N equal."""
     from m3s.config import config
     from m3s.frame import Frame, Keyframes
     from m3s.sim3 import Sim3
@@ -323,11 +325,11 @@ def test_track_sequence_matches_reference_run(golden):
     from m3s.tracker import FrameTracker
 
     g = golden("track_seq.npz")
-    H, W = (int(v) for v in g["S1_shape"])
+    H, W = (int(v) for v in g[f"{case}_shape"])
     dev = torch.device("cuda")
-    pairs = [make_pair(H, W, seed=int(s)) for s in g["S1_seeds"]]
+    pairs = [make_pair(H, W, seed=int(s)) for s in g[f"{case}_seeds"]]
     saved = config["use_calib"]
-    config["use_calib"] = True
+    config["use_calib"] = bool(g[f"{case}_calib"])
     try:
         kf = Frame(0, (H, W), T_WC=Sim3.Identity(1, device=dev))
         kf.K = pairs[0]["K"].to(dev)
@@ -342,18 +344,19 @@ def test_track_sequence_matches_reference_run(golden):
             assert not reloc
             T = fr.T_WC
             Tf = T.data.reshape(-1).cpu().numpy()
-            print(f"S1 frame {k}: pose err vs the reference run {np.abs(Tf - g[f'S1_f{k}_T_WCf'][0]).max():.2e}, "
-                  f"iters {tr.last_result.iters} / {int(g[f'S1_f{k}_iters'])}")
-            assert tr.last_result.iters == int(g[f"S1_f{k}_iters"])
-            assert new_kf == bool(g[f"S1_f{k}_new_kf"])
-            np.testing.assert_allclose(Tf, g[f"S1_f{k}_T_WCf"][0], atol=1e-5)
+            print(f"{case} frame {k}: pose err vs the reference run {np.abs(Tf - g[f'{case}_f{k}_T_WCf'][0]).max():.2e}, "
+                  f"iters {tr.last_result.iters} / {int(g[f'{case}_f{k}_iters'])}")
+            assert tr.last_result.iters == int(g[f"{case}_f{k}_iters"])
+            assert new_kf == bool(g[f"{case}_f{k}_new_kf"])
+            np.testing.assert_allclose(Tf, g[f"{case}_f{k}_T_WCf"][0], atol=1e-5)
         kfin = kfs[0]
-        sub = torch.from_numpy(g["S1_sub"]).to(dev)
-        assert kfin.N == int(g["S1_kf_N"])
+        sub = torch.from_numpy(g[f"{case}_sub"]).to(dev)
+        assert kfin.N == int(g[f"{case}_kf_N"])
         kX = kfin.X_canon[sub].cpu().numpy()
         kC = kfin.C[sub].cpu().numpy()
-        print(f"S1 keyframe: X err {np.abs(kX - g['S1_kf_X_sub']).max():.2e}, C err {np.abs(kC - g['S1_kf_C_sub']).max():.2e}")
-        np.testing.assert_allclose(kX, g["S1_kf_X_sub"], atol=1e-5, rtol=1e-5)
-        np.testing.assert_allclose(kC, g["S1_kf_C_sub"], rtol=1e-6)
+        print(f"{case} keyframe: X err {np.abs(kX - g[f'{case}_kf_X_sub']).max():.2e}, "
+              f"C err {np.abs(kC - g[f'{case}_kf_C_sub']).max():.2e}")
+        np.testing.assert_allclose(kX, g[f"{case}_kf_X_sub"], atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(kC, g[f"{case}_kf_C_sub"], rtol=1e-6)
     finally:
         config["use_calib"] = saved

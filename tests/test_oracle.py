@@ -220,28 +220,29 @@ def test_batched_warm_match_restatement_matches_reference(golden):
         assert dig(v) == str(g[f"C3w_{k}_sha256"]), f"C3w {k} differs from the reference run"
 
 
-def test_track_sequence_restatement_matches_reference(golden):
-    """S1: three frames tracked in sequence against one keyframe at the bench's headline shape (512x512 calib, the
-    bench's pairs, idx_f2k warm start, each frame starting at the previous pose, weighted_pointmap fusion
-    accumulating), the oracle chain (tests/track_chain.py oracle_track_seq) against the reference's own
-    FrameTracker.track run (gen_track_seq): GN step counts and new_kf equal, poses and the fused keyframe within
-    the 1e-5 contract."""
+@pytest.mark.parametrize("case", ["S1", "S2"])
+def test_track_sequence_restatement_matches_reference(golden, case):
+    """Three frames tracked in sequence against one keyframe at the bench's shape (512x512, the bench's pairs,
+    idx_f2k warm start, each frame starting at the previous pose, weighted_pointmap fusion accumulating); S1 calib
+    (the headline mode), S2 rays. The oracle chain (tests/track_chain.py oracle_track_seq) against the reference's
+    own FrameTracker.track run (gen_track_seq): GN step counts and new_kf equal, poses and the fused keyframe
+    within the 1e-5 contract."""
     from m3s.synthetic import make_pair
     from track_chain import oracle_track_seq
 
     g = golden("track_seq.npz")
-    H, W = (int(v) for v in g["S1_shape"])
-    pairs = [make_pair(H, W, seed=int(s)) for s in g["S1_seeds"]]
-    frames, kX, kC, kN = oracle_track_seq(pairs, H, W)
-    sub = g["S1_sub"]
+    H, W = (int(v) for v in g[f"{case}_shape"])
+    pairs = [make_pair(H, W, seed=int(s)) for s in g[f"{case}_seeds"]]
+    frames, kX, kC, kN = oracle_track_seq(pairs, H, W, "calib" if bool(g[f"{case}_calib"]) else "rays")
+    sub = g[f"{case}_sub"]
     for k, (Tf, it, new_kf) in enumerate(frames):
-        print(f"S1 frame {k}: pose err vs the reference run {np.abs(Tf - g[f'S1_f{k}_T_WCf'][0]).max():.2e}, "
-              f"iters {it} / {int(g[f'S1_f{k}_iters'])}")
-        assert it == int(g[f"S1_f{k}_iters"]) and new_kf == bool(g[f"S1_f{k}_new_kf"])
-        np.testing.assert_allclose(Tf, g[f"S1_f{k}_T_WCf"][0], atol=1e-5)
-    assert kN == int(g["S1_kf_N"])
-    np.testing.assert_allclose(kX[sub], g["S1_kf_X_sub"], atol=1e-5, rtol=1e-5)
-    np.testing.assert_allclose(kC[sub], g["S1_kf_C_sub"][:, 0], rtol=1e-6)
+        print(f"{case} frame {k}: pose err vs the reference run {np.abs(Tf - g[f'{case}_f{k}_T_WCf'][0]).max():.2e}, "
+              f"iters {it} / {int(g[f'{case}_f{k}_iters'])}")
+        assert it == int(g[f"{case}_f{k}_iters"]) and new_kf == bool(g[f"{case}_f{k}_new_kf"])
+        np.testing.assert_allclose(Tf, g[f"{case}_f{k}_T_WCf"][0], atol=1e-5)
+    assert kN == int(g[f"{case}_kf_N"])
+    np.testing.assert_allclose(kX[sub], g[f"{case}_kf_X_sub"], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(kC[sub], g[f"{case}_kf_C_sub"][:, 0], rtol=1e-6)
 
 
 @pytest.mark.parametrize("case", ["C1_rays", "C1_calib", "C2_calib"])

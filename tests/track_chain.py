@@ -31,8 +31,8 @@ def oracle_track(P, mode, H, W):
     return idx, valid, Tf, kX, it
 
 
-def oracle_track_seq(pairs, H, W):
-    """tracker.py:28-114 over a sequence of frames against one keyframe, calib mode, on the oracle: each frame
+def oracle_track_seq(pairs, H, W, mode="calib"):
+    """tracker.py:28-114 over a sequence of frames against one keyframe (calib or rays mode) on the oracle: each frame
     matched from the previous frame's idx_f2k (reset on new_kf), started at the previous frame's pose, the keyframe
     fused by weighted_pointmap after every frame (frame.py:74-77: X <- (C X + C' X') / (C + C'), C <- C + C',
     N <- N + 1; the tracker's Ck is the average C / N). Returns [(T_WCf, iters, new_kf)] per frame and the final
@@ -53,12 +53,15 @@ def oracle_track_seq(pairs, H, W):
         Qk = np.sqrt(Q[0].reshape(-1)[i] * Q[1].reshape(-1))
         Ck = (kC / kN).astype(np.float32)
         v = vm & (C[0].reshape(-1)[i] > 0.0) & (Ck > 0.0) & (Qk > 1.5)
-        Xf = O.backproject_constrain(X[0].reshape(1, -1, 3), K, (H, W))[0][i]
         Xk32 = kX.astype(np.float32)
-        z = O.backproject_constrain(Xk32[None], K, (H, W))[0][:, 2]
-        vmk = z > 1e-6
-        meas = np.stack((u.reshape(-1), vv.reshape(-1), np.log(np.where(vmk, z, 1.0))), -1) * vmk[:, None]
-        Tf, Tr, it = O.track_calib(Xf, Xk32, T, I8, Qk, v, meas, vmk, K, (H, W))
+        if mode == "rays":
+            Tf, Tr, it = O.track_rays(X[0].reshape(-1, 3)[i], Xk32, T, I8, Qk, v)
+        else:
+            Xf = O.backproject_constrain(X[0].reshape(1, -1, 3), K, (H, W))[0][i]
+            z = O.backproject_constrain(Xk32[None], K, (H, W))[0][:, 2]
+            vmk = z > 1e-6
+            meas = np.stack((u.reshape(-1), vv.reshape(-1), np.log(np.where(vmk, z, 1.0))), -1) * vmk[:, None]
+            Tf, Tr, it = O.track_calib(Xf, Xk32, T, I8, Qk, v, meas, vmk, K, (H, W))
         valid_kf = vm & (Qk > 1.5)
         n_unique = np.unique(i[vm]).size
         new_kf = min(valid_kf.sum() / i.size, n_unique / i.size) < 0.333
